@@ -1,0 +1,207 @@
+/*
+ * rt.h — C ABI of the MI355X path-tracing kernel library (librt_amd.so).
+ *
+ * Drop-in boundary for the reference's hot path
+ *     raytrace :: ToRandom m => CameraSettings -> Geometry m Material -> StdGen -> A.Matrix D Color
+ *     (UnaryPlus/raytrace src/Graphics/Ray.hs:121-238)
+ * The reference has no FFI of its own (pure Haskell, no `foreign import`); the entry points
+ * below are what its Haskell side binds with `foreign import ccall safe` (INTEGRATION.md shows
+ * the binding).  Plain C types only: no HIP or torch types cross this boundary; device
+ * pointers and streams are passed as `void*` / `float*` owned by the caller.
+ *
+ * Scene contract.  The reference's Geometry / Material / Texture / background are closures
+ * (Geometry.hs:42, Material.hs:17, Texture.hs:15, Ray.hs:57).  The caller reifies them through
+ * a deep embedding of the same smart constructors and passes the FLATTENED scene:
+ *   - every leaf surface (sphere / parallelogram / triangle) with rigid `transform`s baked in,
+ *     its material (outermost `<$` wins), its `moving` motion and its depth-first `order`
+ *     (the reference's closest-hit tie-break: earlier leaf wins on equal t, Geometry.hs:340-361);
+ *   - every `constantMedium` lifted to the top level with its boundary leaves in their own set.
+ * The library builds its own bounding-volume hierarchy over that list; the closest hit (and
+ * therefore the image) does not depend on the tree the caller wrote.
+ *
+ * Output.  Linear RGB, float32, row-major [row][column][rgb] — row 0 is the TOP of the image —
+ * each pixel the MEAN over `samples_per_pixel` samples (Ray.hs:226-232).  Randomness is a
+ * counter-based Philox4x32-10 stream keyed by `seed` and indexed by (pixel, sample, segment,
+ * event), so results are deterministic for a given (scene, camera, seed) and independent of
+ * the shard layout and of the GPU count.
+ */
+#ifndef RT_AMD_H
+#define RT_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* status codes */
+#define RT_OK 0
+#define RT_E_GENERIC (-1)
+#define RT_E_INVALID (-2)      /* malformed scene/camera (reference: `error` / NaN)              */
+#define RT_E_UNSUPPORTED (-3)  /* closure the device cannot evaluate; caller falls back to CPU   */
+#define RT_E_HIP (-4)          /* HIP runtime failure (no device, launch failure, OOM)            */
+#define RT_E_STACK (-5)        /* BVH traversal stack overflow (scene too deep)                   */
+
+/* primitive kinds (Geometry.hs:58-176) */
+#define RT_PRIM_SPHERE 0
+#define RT_PRIM_PARALLELOGRAM 1
+#define RT_PRIM_TRIANGLE 2
+
+/* material kinds (Material.hs:41-129) */
+#define RT_MAT_LIGHT_SOURCE 0
+#define RT_MAT_PITCH_BLACK 1
+#define RT_MAT_LAMBERTIAN 2
+#define RT_MAT_LOMMEL_SEELIGER 3
+#define RT_MAT_MIRROR 4
+#define RT_MAT_METAL 5        /* param = fuzz */
+#define RT_MAT_DIELECTRIC 6   /* param = index of refraction */
+#define RT_MAT_TRANSPARENT 7
+#define RT_MAT_ISOTROPIC 8
+#define RT_MAT_ANISOTROPIC 9  /* param = Henyey-Greenstein g */
+
+/* texture kinds (Texture.hs:18-78) */
+#define RT_TEX_CONSTANT 0     /* c0 */
+#define RT_TEX_CHECKER 1      /* nu, nv, c0, c1 */
+
+/* background kinds (cs_background restricted to reifiable closures) */
+#define RT_BG_CONST 0         /* c0 */
+#define RT_BG_LERP_Y 1        /* (1 - a) c0 + a c1, a = 0.5 (dir.y + 1)  (`sky`, `grayFade`) */
+
+/* One leaf surface.  Ray.hs/Geometry.hs semantics; all coordinates in world space. */
+typedef struct rt_prim {
+  int32_t kind;      /* RT_PRIM_* */
+  int32_t material;  /* index into rt_scene.materials (ignored for medium boundaries)          */
+  int32_t set;       /* 0 = visible surface; k >= 1 = boundary of rt_scene.media[k-1]         */
+  int32_t motion;    /* -1 or index into rt_scene.motions (`moving`, Geometry.hs:449-456)      */
+  int32_t gid;       /* geometric identity: the same source leaf under the same transform has
+                        the same gid in every set (used to skip self-intersection)          */
+  int32_t order;     /* depth-first position of the leaf in the caller's tree (tie-break)     */
+  int32_t uvframe;   /* -1 or index into rt_scene.uvframes: rotation R^T for sphereUV         */
+  int32_t pad;
+  double p[9];       /* sphere: center[3], radius, -; plane: q[3], u[3], v[3]                 */
+  double uv[6];      /* plane shapes: uv0, uv1, uv2 (parallelogram: (0,0),(1,0),(0,1))         */
+} rt_prim;
+
+typedef struct rt_medium {   /* constantMedium (Geometry.hs:298-330) */
+  double density;
+  int32_t material;
+  int32_t order;
+} rt_medium;
+
+typedef struct rt_material {
+  int32_t kind;      /* RT_MAT_* */
+  int32_t texture;   /* index into rt_scene.textures */
+  double param;
+} rt_material;
+
+typedef struct rt_texture {
+  int32_t kind;      /* RT_TEX_* */
+  int32_t nu, nv;    /* checker dimensions */
+  int32_t image;     /* reserved (-1) */
+  double c0[3], c1[3];
+  double params[8];  /* reserved */
+} rt_texture;
+
+typedef struct rt_motion {
+  double v0[3], v1[3];   /* world-space shift (1 - time) v0 + time v1 */
+} rt_motion;
+
+typedef struct rt_uvframe {
+  double r[9];           /* row-major 3x3: object-space normal = r * world-space normal */
+} rt_uvframe;
+
+typedef struct rt_scene {
+  int32_t n_prims;      const rt_prim* prims;
+  int32_t n_media;      const rt_medium* media;
+  int32_t n_materials;  const rt_material* materials;
+  int32_t n_textures;   const rt_texture* textures;
+  int32_t n_motions;    const rt_motion* motions;
+  int32_t n_uvframes;   const rt_uvframe* uvframes;
+} rt_scene;
+
+typedef struct rt_redirect_target {   /* cs_redirectTargets element (p, q, u, v) */
+  double prob;
+  double q[3], u[3], v[3];
+} rt_redirect_target;
+
+/* CameraSettings (Ray.hs:40-68) with the background reified. */
+typedef struct rt_camera_settings {
+  double center[3];
+  double look_at[3];
+  double up[3];
+  double vfov;              /* radians */
+  double aspect_ratio;
+  int32_t image_width;
+  int32_t samples_per_pixel;
+  int32_t max_recursion_depth;
+  int32_t background_kind;  /* RT_BG_* */
+  double background_c0[3];
+  double background_c1[3];
+  double defocus_angle;     /* radians */
+  double focus_dist;
+  int32_t n_redirect_targets;
+  int32_t pad;
+  const rt_redirect_target* redirect_targets;
+} rt_camera_settings;
+
+/* Which rows this call renders.  Rows are dealt to shards in blocks of `row_block`
+ * round-robin: shard r owns global rows y with (y / row_block) % n_shards == r.  Every shard
+ * has the same padded row count (rt_shard_rows); padding rows are written as zeros. */
+typedef struct rt_exec {
+  int32_t device;       /* HIP device ordinal */
+  int32_t n_shards;     /* >= 1 */
+  int32_t shard;        /* 0 .. n_shards-1 */
+  int32_t row_block;    /* >= 1 */
+  int32_t flags;        /* reserved, 0 */
+  int32_t pad;
+} rt_exec;
+
+typedef struct rt_stats {
+  double upload_ms;     /* scene build + host->device copy */
+  double kernel_ms;     /* device time of the render kernel */
+  double total_ms;      /* wall time of the call */
+  int64_t samples;      /* pixels x spp rendered by this call */
+  int32_t bvh_nodes;    /* nodes of all sets */
+  int32_t max_stack;    /* deepest traversal stack the build can require */
+} rt_stats;
+
+typedef struct rt_device_scene rt_device_scene;   /* opaque, device-resident scene */
+
+int rt_abi_version(void);
+const char* rt_last_error(void);   /* thread-local message of the last failing call */
+
+/* image height for a width and aspect ratio: round (w / aspect), banker's rounding (Ray.hs:123) */
+int rt_image_height(const rt_camera_settings* cs);
+/* padded rows per shard for an image of `height` rows under `ex` */
+int rt_shard_rows(int32_t height, const rt_exec* ex);
+/* global row of shard-local row t (may be >= height for padding rows) */
+int rt_shard_row(int32_t t, const rt_exec* ex);
+
+/* One-shot host-buffer call — the Haskell binding's entry point (replaces Ray.hs:121-238).
+ * out_rgb: caller-owned host buffer of rt_shard_rows(h, ex) * image_width * 3 floats
+ * (the whole image when n_shards == 1).  Returns RT_OK or a negative RT_E_* code. */
+int rt_render(const rt_camera_settings* cs, const rt_scene* scene, uint64_t seed, const rt_exec* ex,
+              float* out_rgb, rt_stats* stats);
+
+/* Device-resident path (used when inputs already live in HBM, e.g. bench.py / torch callers). */
+int rt_scene_create(const rt_scene* scene, int32_t device, rt_device_scene** out);
+int rt_scene_destroy(rt_device_scene* s);
+int rt_scene_stats(const rt_device_scene* s, rt_stats* stats);
+/* Enqueue one render on `hip_stream` (a hipStream_t, or NULL for the default stream).
+ * d_out_rgb: device buffer of rt_shard_rows(h, ex) * image_width * 3 floats.  Asynchronous;
+ * the scene must outlive the work. */
+int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex,
+                    float* d_out_rgb, void* hip_stream);
+
+/* Fused output epilogue of writeImage / writeImageSqrt (Ray.hs:248-260): linear float RGB ->
+ * 8-bit codes min(255, floor(256 * transfer(clamp01 x))), transfer = sRGB (encoding 0) or
+ * sqrt (encoding 1).  Device pointers, asynchronous on hip_stream. */
+int rt_encode8_async(const float* d_rgb, uint8_t* d_out, int64_t n_values, int32_t encoding, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_AMD_H */

@@ -1,0 +1,235 @@
+// rt_api.hip — the C-ABI entry points of include/rt.h: scene build (rt_build.cpp), upload to
+// HBM, kernel launch (rt_kernel.hip), error reporting.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt.h"
+#include "rt_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) return fail(RT_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+int upload(T** dst, const std::vector<T>& src) {
+  size_t bytes = src.size() * sizeof(T);
+  HIP_TRY(hipMalloc((void**)dst, bytes ? bytes : 16));
+  if (bytes) HIP_TRY(hipMemcpy(*dst, src.data(), bytes, hipMemcpyHostToDevice));
+  return RT_OK;
+}
+
+}  // namespace
+
+struct rt_device_scene {
+  int device = 0;
+  float* nodes = nullptr;
+  float* prims = nullptr;
+  int* prim_mat = nullptr;
+  float* prim_uv = nullptr;
+  DevMaterial* mats = nullptr;
+  DevTexture* texs = nullptr;
+  float* motions = nullptr;
+  float* uvframes = nullptr;
+  int* status = nullptr;
+  int surface_root = RT_EMPTY_ROOT;
+  int n_media = 0;
+  DevMedium media[RT_MAX_MEDIA];
+  int n_nodes = 0, n_prims = 0, max_depth = 0;
+  double upload_ms = 0;
+};
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+const char* rt_last_error(void) { return g_err.c_str(); }
+
+int rt_image_height(const rt_camera_settings* cs) {
+  if (!cs) return fail(RT_E_INVALID, "null camera settings");
+  int h = rt_host_image_height(cs);
+  if (h < 0) return fail(RT_E_INVALID, "image height is not finite");
+  return h;
+}
+
+int rt_shard_rows(int32_t height, const rt_exec* ex) {
+  int r = rt_host_shard_rows(height, ex);
+  if (r < 0) return fail(RT_E_INVALID, "invalid rt_exec");
+  return r;
+}
+
+int rt_shard_row(int32_t t, const rt_exec* ex) {
+  if (!ex || ex->n_shards < 1 || ex->row_block < 1) return fail(RT_E_INVALID, "invalid rt_exec");
+  return ((t / ex->row_block) * ex->n_shards + ex->shard) * ex->row_block + (t % ex->row_block);
+}
+
+int rt_scene_destroy(rt_device_scene* s) {
+  if (!s) return RT_OK;
+  (void)hipSetDevice(s->device);
+  (void)hipFree(s->nodes);
+  (void)hipFree(s->prims);
+  (void)hipFree(s->prim_mat);
+  (void)hipFree(s->prim_uv);
+  (void)hipFree(s->mats);
+  (void)hipFree(s->texs);
+  (void)hipFree(s->motions);
+  (void)hipFree(s->uvframes);
+  (void)hipFree(s->status);
+  delete s;
+  return RT_OK;
+}
+
+int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!sc || !out) return fail(RT_E_INVALID, "null argument");
+  *out = nullptr;
+  HostScene H;
+  std::string err;
+  int rc = rt_host_build_scene(sc, H, err);
+  if (rc) return fail(rc, "%s", err.c_str());
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RT_E_HIP, "no HIP device");
+  if (device < 0 || device >= ndev) return fail(RT_E_INVALID, "device %d out of range (%d devices)", device, ndev);
+  HIP_TRY(hipSetDevice(device));
+  auto* s = new rt_device_scene();
+  s->device = device;
+  std::vector<int> status(4, 0);
+  if ((rc = upload(&s->nodes, H.nodes)) || (rc = upload(&s->prims, H.prims)) ||
+      (rc = upload(&s->prim_mat, H.prim_mat)) || (rc = upload(&s->prim_uv, H.prim_uv)) ||
+      (rc = upload(&s->mats, H.mats)) || (rc = upload(&s->texs, H.texs)) || (rc = upload(&s->motions, H.motions)) ||
+      (rc = upload(&s->uvframes, H.uvframes)) || (rc = upload(&s->status, status))) {
+    rt_scene_destroy(s);
+    return rc;
+  }
+  s->surface_root = H.surface_root;
+  s->n_media = H.n_media;
+  for (int k = 0; k < H.n_media; ++k) s->media[k] = H.media[k];
+  s->n_nodes = H.n_nodes;
+  s->n_prims = H.n_prims;
+  s->max_depth = H.max_depth;
+  s->upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *out = s;
+  return RT_OK;
+}
+
+int rt_scene_stats(const rt_device_scene* s, rt_stats* st) {
+  if (!s || !st) return fail(RT_E_INVALID, "null argument");
+  std::memset(st, 0, sizeof *st);
+  st->upload_ms = s->upload_ms;
+  st->bvh_nodes = s->n_nodes;
+  st->max_stack = s->max_depth;
+  return RT_OK;
+}
+
+int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex,
+                    float* d_out_rgb, void* hip_stream) {
+  if (!s || !d_out_rgb) return fail(RT_E_INVALID, "null argument");
+  KernelParams P;
+  std::memset(&P, 0, sizeof P);
+  std::string err;
+  int rc = rt_host_make_params(cs, seed, ex, P, err);
+  if (rc) return fail(rc, "%s", err.c_str());
+  P.nodes = s->nodes;
+  P.prims = s->prims;
+  P.prim_mat = s->prim_mat;
+  P.prim_uv = s->prim_uv;
+  P.mats = s->mats;
+  P.texs = s->texs;
+  P.motions = s->motions;
+  P.uvframes = s->uvframes;
+  P.status = s->status;
+  P.out = d_out_rgb;
+  P.surface_root = s->surface_root;
+  P.n_media = s->n_media;
+  for (int k = 0; k < s->n_media; ++k) P.media[k] = s->media[k];
+  HIP_TRY(hipSetDevice(s->device));
+  if (rt_launch_render(P, hip_stream))
+    return fail(RT_E_HIP, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return RT_OK;
+}
+
+int rt_render(const rt_camera_settings* cs, const rt_scene* scene, uint64_t seed, const rt_exec* ex, float* out_rgb,
+              rt_stats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!cs || !scene || !ex || !out_rgb) return fail(RT_E_INVALID, "null argument");
+  int h = rt_host_image_height(cs);
+  if (h <= 0 || cs->image_width <= 0) return fail(RT_E_INVALID, "image %dx%d must be non-empty", cs->image_width, h);
+  int rows = rt_host_shard_rows(h, ex);
+  if (rows < 0) return fail(RT_E_INVALID, "invalid rt_exec");
+  {  // validate the camera before touching the device
+    KernelParams P;
+    std::string err;
+    int rc = rt_host_make_params(cs, seed, ex, P, err);
+    if (rc) return fail(rc, "%s", err.c_str());
+  }
+  rt_device_scene* s = nullptr;
+  int rc = rt_scene_create(scene, ex->device, &s);
+  if (rc) return rc;
+  size_t bytes = (size_t)rows * cs->image_width * 3 * sizeof(float);
+  float* d_out = nullptr;
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int status = 0;
+  float ms = 0;
+  if (hipMalloc((void**)&d_out, bytes ? bytes : 16) != hipSuccess) rc = fail(RT_E_HIP, "hipMalloc(%zu) failed", bytes);
+  if (!rc && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) rc = fail(RT_E_HIP, "stream create");
+  if (!rc && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) rc = fail(RT_E_HIP, "events");
+  if (!rc) {
+    (void)hipEventRecord(e0, st);
+    rc = rt_render_async(s, cs, seed, ex, d_out, st);
+    (void)hipEventRecord(e1, st);
+  }
+  if (!rc && hipStreamSynchronize(st) != hipSuccess)
+    rc = fail(RT_E_HIP, "render failed: %s", hipGetErrorString(hipGetLastError()));
+  if (!rc) (void)hipEventElapsedTime(&ms, e0, e1);
+  if (!rc && hipMemcpy(out_rgb, d_out, bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(RT_E_HIP, "copy back");
+  if (!rc && hipMemcpy(&status, s->status, 4, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(RT_E_HIP, "status");
+  if (!rc && status) rc = fail(RT_E_STACK, "BVH traversal stack overflow");
+  if (stats && !rc) {
+    std::memset(stats, 0, sizeof *stats);
+    stats->upload_ms = s->upload_ms;
+    stats->kernel_ms = ms;
+    stats->samples = (int64_t)rows * cs->image_width * cs->samples_per_pixel;
+    stats->bvh_nodes = s->n_nodes;
+    stats->max_stack = s->max_depth;
+    stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (st) (void)hipStreamDestroy(st);
+  (void)hipFree(d_out);
+  rt_scene_destroy(s);
+  return rc;
+}
+
+int rt_encode8_async(const float* d_rgb, uint8_t* d_out, int64_t n_values, int32_t encoding, void* hip_stream) {
+  if (!d_rgb || !d_out || n_values < 0) return fail(RT_E_INVALID, "invalid encode arguments");
+  if (encoding != 0 && encoding != 1) return fail(RT_E_INVALID, "encoding must be 0 (sRGB) or 1 (sqrt)");
+  if (rt_launch_encode8(d_rgb, d_out, n_values, encoding, hip_stream))
+    return fail(RT_E_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,319 @@
+// rt_build.cpp — host-side scene image and launch parameters (no HIP calls).
+//
+//  * validates the flattened scene of include/rt.h,
+//  * precomputes the plane-shape frame of Geometry.hs:117-131 (unit normal n, and the
+//    vectors wa = v x nS, wb = nS x u so that a = nS.((p-q) x v) = (p-q).wa and
+//    b = nS.(u x (p-q)) = (p-q).wb) in binary64 and rounds it once to FP32,
+//  * builds one BVH per primitive set (surfaces, then each medium's boundary),
+//  * evaluates the camera set-up of Ray.hs:122-155 in binary64, in the reference's order.
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/rt.h"
+#include "rt_bvh.h"
+#include "rt_internal.h"
+
+namespace {
+
+struct d3 {
+  double x, y, z;
+};
+inline d3 D3(const double* p) { return {p[0], p[1], p[2]}; }
+inline d3 operator+(d3 a, d3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline d3 operator-(d3 a, d3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline d3 operator-(d3 a) { return {-a.x, -a.y, -a.z}; }
+inline d3 smul(double s, d3 a) { return {s * a.x, s * a.y, s * a.z}; }
+inline d3 divs(d3 a, double s) { return {a.x / s, a.y / s, a.z / s}; }
+inline double dot(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline d3 cross(d3 a, d3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+inline d3 normalize_hs(d3 v) {  // linear's normalize
+  double l = dot(v, v);
+  if (std::fabs(l) <= 1e-12 || std::fabs(1 - l) <= 1e-12) return v;
+  return divs(v, std::sqrt(l));
+}
+inline void put3(float* dst, d3 v) {
+  dst[0] = (float)v.x;
+  dst[1] = (float)v.y;
+  dst[2] = (float)v.z;
+}
+inline bool finite_n(const double* p, int n) {
+  for (int i = 0; i < n; ++i)
+    if (!std::isfinite(p[i])) return false;
+  return true;
+}
+inline float ibits(int v) {
+  float f;
+  std::memcpy(&f, &v, 4);
+  return f;
+}
+
+int fail(std::string& err, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
+int fail(std::string& err, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  err = buf;
+  return code;
+}
+
+}  // namespace
+
+int rt_host_image_height(const rt_camera_settings* cs) {
+  double h = (double)cs->image_width / cs->aspect_ratio;
+  if (!std::isfinite(h) || h > 1e9) return -1;
+  return (int)std::nearbyint(h);  // round-half-even under the default rounding mode (Ray.hs:123)
+}
+
+int rt_host_shard_rows(int height, const rt_exec* ex) {
+  if (!ex || ex->n_shards < 1 || ex->row_block < 1 || ex->shard < 0 || ex->shard >= ex->n_shards || height < 0)
+    return RT_E_INVALID;
+  int blocks = (height + ex->row_block - 1) / ex->row_block;
+  int per = (blocks + ex->n_shards - 1) / ex->n_shards;
+  return per * ex->row_block;
+}
+
+int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
+  if (!sc) return fail(err, RT_E_INVALID, "null scene");
+  if (sc->n_prims < 0 || sc->n_media < 0 || sc->n_materials < 0 || sc->n_textures < 0 || sc->n_motions < 0 ||
+      sc->n_uvframes < 0)
+    return fail(err, RT_E_INVALID, "negative count");
+  if (sc->n_media > RT_MAX_MEDIA)
+    return fail(err, RT_E_UNSUPPORTED, "%d media (at most %d)", sc->n_media, RT_MAX_MEDIA);
+  if ((sc->n_prims && !sc->prims) || (sc->n_media && !sc->media) || (sc->n_materials && !sc->materials) ||
+      (sc->n_textures && !sc->textures) || (sc->n_motions && !sc->motions) || (sc->n_uvframes && !sc->uvframes))
+    return fail(err, RT_E_INVALID, "null array with nonzero count");
+  for (int i = 0; i < sc->n_textures; ++i) {
+    const rt_texture& t = sc->textures[i];
+    if (t.kind != RT_TEX_CONSTANT && t.kind != RT_TEX_CHECKER)
+      return fail(err, RT_E_UNSUPPORTED, "texture %d: kind %d is not evaluated on the device", i, t.kind);
+    if (!finite_n(t.c0, 3) || !finite_n(t.c1, 3)) return fail(err, RT_E_INVALID, "texture %d: non-finite colour", i);
+  }
+  for (int i = 0; i < sc->n_materials; ++i) {
+    const rt_material& m = sc->materials[i];
+    if (m.kind < 0 || m.kind > RT_MAT_ANISOTROPIC)
+      return fail(err, RT_E_UNSUPPORTED, "material %d: kind %d", i, m.kind);
+    if (m.texture < 0 || m.texture >= sc->n_textures)
+      return fail(err, RT_E_INVALID, "material %d: bad texture index", i);
+  }
+  for (int k = 0; k < sc->n_media; ++k) {
+    const rt_medium& m = sc->media[k];
+    if (!(m.density > 0) || !std::isfinite(m.density))
+      return fail(err, RT_E_INVALID, "medium %d: density must be > 0", k);
+    if (m.material < 0 || m.material >= sc->n_materials) return fail(err, RT_E_INVALID, "medium %d: bad material", k);
+  }
+  const int n_sets = 1 + sc->n_media;
+  std::vector<std::vector<BuildPrim>> sets(n_sets);
+  for (int i = 0; i < sc->n_prims; ++i) {
+    const rt_prim& p = sc->prims[i];
+    if (p.kind < RT_PRIM_SPHERE || p.kind > RT_PRIM_TRIANGLE) return fail(err, RT_E_INVALID, "prim %d: bad kind", i);
+    if (p.set < 0 || p.set >= n_sets) return fail(err, RT_E_INVALID, "prim %d: bad set %d", i, p.set);
+    if (p.set == 0 && (p.material < 0 || p.material >= sc->n_materials))
+      return fail(err, RT_E_INVALID, "prim %d: surface without a valid material", i);
+    if (p.motion >= sc->n_motions || p.uvframe >= sc->n_uvframes)
+      return fail(err, RT_E_INVALID, "prim %d: bad motion/uvframe index", i);
+    if (!finite_n(p.p, p.kind == RT_PRIM_SPHERE ? 4 : 9))
+      return fail(err, RT_E_INVALID, "prim %d: non-finite geometry", i);
+    BuildPrim bp;
+    bp.index = i;
+    if (p.kind == RT_PRIM_SPHERE) {
+      double r = std::fabs(p.p[3]);
+      for (int a = 0; a < 3; ++a) {
+        bp.lo[a] = p.p[a] - r;
+        bp.hi[a] = p.p[a] + r;
+      }
+    } else {
+      for (int a = 0; a < 3; ++a) {
+        double q = p.p[a], u = p.p[3 + a], v = p.p[6 + a];
+        double c[4] = {q, q + u, q + v, q + u + v};
+        int nc = p.kind == RT_PRIM_PARALLELOGRAM ? 4 : 3;
+        bp.lo[a] = bp.hi[a] = c[0];
+        for (int k = 1; k < nc; ++k) {
+          bp.lo[a] = std::fmin(bp.lo[a], c[k]);
+          bp.hi[a] = std::fmax(bp.hi[a], c[k]);
+        }
+      }
+    }
+    if (p.motion >= 0) {
+      const rt_motion& m = sc->motions[p.motion];
+      if (!finite_n(m.v0, 3) || !finite_n(m.v1, 3)) return fail(err, RT_E_INVALID, "motion %d non-finite", p.motion);
+      for (int a = 0; a < 3; ++a) {
+        double lo = bp.lo[a], hi = bp.hi[a];
+        bp.lo[a] = std::fmin(lo + m.v0[a], lo + m.v1[a]);
+        bp.hi[a] = std::fmax(hi + m.v0[a], hi + m.v1[a]);
+      }
+    }
+    sets[p.set].push_back(bp);
+  }
+  for (int k = 0; k < sc->n_media; ++k)
+    if (sets[k + 1].empty()) return fail(err, RT_E_INVALID, "medium %d has an empty boundary", k);
+
+  // one BVH per set; primitives stored in leaf order, set after set
+  std::vector<int> order;
+  std::vector<int> roots(n_sets);
+  S.nodes.clear();
+  S.max_depth = 0;
+  for (int s = 0; s < n_sets; ++s) {
+    BvhOut bo;
+    rt_build_bvh(sets[s], (int)(S.nodes.size() / 16), (int)order.size(), bo);
+    S.nodes.insert(S.nodes.end(), bo.nodes.begin(), bo.nodes.end());
+    order.insert(order.end(), bo.order.begin(), bo.order.end());
+    roots[s] = bo.root;
+    S.max_depth = std::max(S.max_depth, bo.max_depth);
+  }
+  if (S.max_depth > RT_STACK_DEPTH)
+    return fail(err, RT_E_STACK, "BVH depth %d exceeds the traversal stack (%d)", S.max_depth, RT_STACK_DEPTH);
+  const int n = (int)order.size();
+  S.prims.assign((size_t)n * 16, 0.0f);
+  S.prim_mat.assign(n, -1);
+  S.prim_uv.assign((size_t)n * 6, 0.0f);
+  for (int j = 0; j < n; ++j) {
+    const rt_prim& p = sc->prims[order[j]];
+    float* f = S.prims.data() + 16 * (size_t)j;
+    int kf = (p.kind == RT_PRIM_SPHERE ? 0 : p.kind == RT_PRIM_PARALLELOGRAM ? 1 : 2) |
+             (p.motion >= 0 ? RT_FLAG_MOTION : 0);
+    if (p.kind == RT_PRIM_SPHERE) {
+      f[0] = (float)p.p[0];
+      f[1] = (float)p.p[1];
+      f[2] = (float)p.p[2];
+      f[4] = (float)p.p[3];
+      f[5] = (float)(p.p[3] * p.p[3]);
+      f[6] = ibits(p.uvframe);
+    } else {
+      d3 q = D3(p.p), u = D3(p.p + 3), v = D3(p.p + 6);
+      d3 cp = cross(u, v);
+      double ncp = std::sqrt(dot(cp, cp));
+      d3 nrm = divs(cp, ncp), nS = divs(nrm, ncp);
+      put3(f, nrm);
+      put3(f + 4, q);
+      put3(f + 8, cross(v, nS));
+      put3(f + 12, cross(nS, u));
+      if (!(ncp > 0)) f[0] = f[1] = f[2] = 0.0f;  // the reference's normal is NaN: never hit
+      for (int k = 0; k < 6; ++k) S.prim_uv[6 * (size_t)j + k] = (float)p.uv[k];
+    }
+    f[3] = ibits(kf);
+    f[7] = ibits(p.gid);
+    f[11] = ibits(p.order);
+    f[15] = ibits(p.motion);
+    S.prim_mat[j] = p.set == 0 ? p.material : -1;
+  }
+  S.mats.assign(sc->n_materials, DevMaterial{});
+  for (int i = 0; i < sc->n_materials; ++i) {
+    S.mats[i].kind = sc->materials[i].kind;
+    S.mats[i].tex = sc->materials[i].texture;
+    S.mats[i].param = (float)sc->materials[i].param;
+  }
+  S.texs.assign(sc->n_textures, DevTexture{});
+  for (int i = 0; i < sc->n_textures; ++i) {
+    const rt_texture& t = sc->textures[i];
+    DevTexture& d = S.texs[i];
+    d.kind = t.kind;
+    d.nu = t.nu;
+    d.nv = t.nv;
+    for (int a = 0; a < 3; ++a) {
+      d.c0[a] = (float)t.c0[a];
+      d.c1[a] = (float)t.c1[a];
+    }
+  }
+  S.motions.assign((size_t)sc->n_motions * 8, 0.0f);
+  for (int i = 0; i < sc->n_motions; ++i)
+    for (int a = 0; a < 3; ++a) {
+      S.motions[8 * (size_t)i + a] = (float)sc->motions[i].v0[a];
+      S.motions[8 * (size_t)i + 4 + a] = (float)sc->motions[i].v1[a];
+    }
+  S.uvframes.assign((size_t)sc->n_uvframes * 12, 0.0f);
+  for (int i = 0; i < sc->n_uvframes; ++i)
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) S.uvframes[12 * (size_t)i + 4 * r + c] = (float)sc->uvframes[i].r[3 * r + c];
+  S.surface_root = roots[0];
+  S.n_media = sc->n_media;
+  for (int k = 0; k < sc->n_media; ++k) {
+    S.media[k].neg_inv_density = (float)(-(1.0 / sc->media[k].density));
+    S.media[k].material = sc->media[k].material;
+    S.media[k].root = roots[k + 1];
+    S.media[k].pad = 0;
+  }
+  S.n_nodes = (int)(S.nodes.size() / 16);
+  S.n_prims = n;
+  return RT_OK;
+}
+
+int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex, KernelParams& P,
+                        std::string& err) {
+  if (!cs || !ex) return fail(err, RT_E_INVALID, "null argument");
+  if (cs->image_width <= 0) return fail(err, RT_E_INVALID, "image width must be positive");
+  if (cs->samples_per_pixel <= 0) return fail(err, RT_E_INVALID, "samples per pixel must be positive");
+  if (!(cs->aspect_ratio > 0)) return fail(err, RT_E_INVALID, "aspect ratio must be positive");
+  int h = rt_host_image_height(cs);
+  if (h <= 0) return fail(err, RT_E_INVALID, "image height %d must be positive", h);
+  if (cs->background_kind != RT_BG_CONST && cs->background_kind != RT_BG_LERP_Y)
+    return fail(err, RT_E_UNSUPPORTED, "background kind %d", cs->background_kind);
+  if (cs->n_redirect_targets < 0 || cs->n_redirect_targets > RT_MAX_TARGETS)
+    return fail(err, RT_E_UNSUPPORTED, "%d redirect targets (at most %d)", cs->n_redirect_targets, RT_MAX_TARGETS);
+  if (cs->n_redirect_targets && !cs->redirect_targets) return fail(err, RT_E_INVALID, "null redirect targets");
+  if (!finite_n(cs->center, 3) || !finite_n(cs->look_at, 3) || !finite_n(cs->up, 3) || !std::isfinite(cs->vfov) ||
+      !std::isfinite(cs->focus_dist) || !std::isfinite(cs->defocus_angle))
+    return fail(err, RT_E_INVALID, "non-finite camera settings");
+  int rows = rt_host_shard_rows(h, ex);
+  if (rows < 0) return fail(err, RT_E_INVALID, "invalid rt_exec");
+  // Ray.hs:122-136, 153-155 in binary64, rounded once to FP32
+  d3 center = D3(cs->center), look = D3(cs->look_at), up = D3(cs->up);
+  double vh = cs->focus_dist * std::tan(cs->vfov / 2) * 2;
+  double vw = vh * (double)cs->image_width / (double)h;
+  d3 w = normalize_hs(center - look);
+  d3 u = normalize_hs(cross(up, w));
+  d3 v = cross(w, u);
+  d3 across = smul(vw, u);
+  d3 down = -smul(vh, v);
+  d3 top_left = ((center - smul(cs->focus_dist, w)) - divs(across, 2)) - divs(down, 2);
+  double dr = cs->focus_dist * std::tan(cs->defocus_angle / 2);
+  std::memset(&P.cam, 0, sizeof P.cam);
+  put3(P.cam.center, center);
+  put3(P.cam.top_left, top_left);
+  put3(P.cam.pixel_u, divs(across, (double)cs->image_width));
+  put3(P.cam.pixel_v, divs(down, (double)h));
+  put3(P.cam.disk_u, smul(dr, u));
+  put3(P.cam.disk_v, smul(dr, v));
+  put3(P.cam.bg0, D3(cs->background_c0));
+  put3(P.cam.bg1, D3(cs->background_c1));
+  P.cam.width = cs->image_width;
+  P.cam.height = h;
+  P.cam.spp = cs->samples_per_pixel;
+  P.cam.max_depth = cs->max_recursion_depth;
+  P.cam.bg_kind = cs->background_kind;
+  // redirect targets (Ray.hs:138-151)
+  double cum = 0, psum = 0;
+  P.n_targets = cs->n_redirect_targets;
+  std::memset(P.targets, 0, sizeof P.targets);
+  for (int k = 0; k < cs->n_redirect_targets; ++k) {
+    const rt_redirect_target& t = cs->redirect_targets[k];
+    DevTarget& T = P.targets[k];
+    d3 q = D3(t.q), uu = D3(t.u), vv = D3(t.v);
+    d3 cp = cross(uu, vv);
+    double ncp = std::sqrt(dot(cp, cp));
+    if (!(ncp > 0) || !std::isfinite(t.prob)) return fail(err, RT_E_INVALID, "redirect target %d is degenerate", k);
+    d3 nrm = divs(cp, ncp), nS = divs(nrm, ncp);
+    put3(T.q, q);
+    put3(T.u, uu);
+    put3(T.v, vv);
+    put3(T.n, nrm);
+    put3(T.wa, cross(vv, nS));
+    put3(T.wb, cross(nS, uu));
+    put3(T.cr, cp);
+    cum = (k == 0) ? t.prob : cum + t.prob;
+    psum = (k == 0) ? t.prob : psum + t.prob;
+    T.prob = (float)t.prob;
+    T.thresh = (float)cum;
+  }
+  P.rem_prob = (float)(1.0 - psum);
+  P.key0 = (uint32_t)seed;
+  P.key1 = (uint32_t)(seed >> 32);
+  P.n_shards = ex->n_shards;
+  P.shard = ex->shard;
+  P.row_block = ex->row_block;
+  P.tile_rows = rows;
+  return RT_OK;
+}

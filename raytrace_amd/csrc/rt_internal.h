@@ -1,0 +1,128 @@
+// rt_internal.h — device-side layout shared by the host scene builder (rt_build.cpp), the
+// C-ABI (rt_api.hip) and the render kernel (rt_kernel.hip / rt_trace.h).  Not part of the
+// public ABI (include/rt.h).  Plain C++ (no HIP types) so the builder compiles anywhere.
+//
+// HBM layout (16-B records, read with one dwordx4 load per lane):
+//   nodes   : 4 x float4 per BVH2 node, both children's boxes in the parent
+//               [0] = (L.lo.x, L.hi.x, L.lo.y, L.hi.y)
+//               [1] = (R.lo.x, R.hi.x, R.lo.y, R.hi.y)
+//               [2] = (L.lo.z, L.hi.z, R.lo.z, R.hi.z)
+//               [3] = (left child, right child, -, -) as int bits; child >= 0 is a node,
+//                     child < 0 is a leaf ~(first * 16 + count - 1)
+//   prims   : 4 x float4 per primitive (reordered into BVH leaf order, set after set)
+//               plane : [0] = (n.xyz, kindflags) [1] = (q.xyz, gid) [2] = (wa.xyz, order)
+//                       [3] = (wb.xyz, motion)   with a = (p-q).wa, b = (p-q).wb (Geometry.hs:130-131)
+//               sphere: [0] = (c.xyz, kindflags) [1] = (radius, radius^2, uvframe, gid)
+//                       [2] = (-, -, -, order)   [3] = (-, -, -, motion)
+//   prim_mat: int per primitive (material index, or -1 for medium boundaries)
+//   prim_uv : 6 floats per primitive (plane shapes' uv0/uv1/uv2)
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#define RT_BLOCK 256
+#define RT_STACK_DEPTH 32
+#define RT_MAX_MEDIA 8
+#define RT_MAX_TARGETS 8
+#define RT_LEAF_MAX 8
+#define RT_EMPTY_ROOT ((int)0x80000000)
+
+#define RT_KIND_MASK 3
+#define RT_FLAG_MOTION 4
+
+// Philox event ids (the oracle uses the same: oracle/rt_oracle.c EV_*)
+#define RT_EV_CAMERA0 0u
+#define RT_EV_CAMERA1 1u
+#define RT_EV_SCATTER 2u
+#define RT_EV_MEDIA 3u
+
+struct DevMaterial {
+  int kind;
+  int tex;
+  float param;
+  int pad;
+};
+
+struct DevTexture {
+  int kind, nu, nv, pad;
+  float c0[3];
+  float c1[3];
+  float pad2[2];
+};
+
+struct DevMedium {
+  float neg_inv_density;  // -(1 / density)  (Geometry.hs:303)
+  int material;
+  int root;               // BVH root of the boundary set
+  int pad;
+};
+
+struct DevTarget {
+  float q[3], u[3], v[3];
+  float n[3];     // unit normal of u x v
+  float wa[3];    // v x nS
+  float wb[3];    // nS x u
+  float cr[3];    // u x v (pdf denominator, Ray.hs:202)
+  float prob;
+  float thresh;   // cumulative probability (scanl1 (+) probs)
+  float pad;
+};
+
+struct DevCamera {
+  float center[3], top_left[3], pixel_u[3], pixel_v[3], disk_u[3], disk_v[3];
+  float bg0[3], bg1[3];
+  int width, height, spp, max_depth, bg_kind;
+  int pad;
+};
+
+struct KernelParams {
+  const float* nodes;      // 16 floats per node
+  const float* prims;      // 16 floats per primitive
+  const int* prim_mat;
+  const float* prim_uv;    // 6 floats per primitive
+  const DevMaterial* mats;
+  const DevTexture* texs;
+  const float* motions;    // 8 floats per motion: v0.xyz, -, v1.xyz, -
+  const float* uvframes;   // 12 floats per frame: rows of R (xyz, -)
+  float* out;
+  int* status;             // device word: nonzero on stack overflow
+  int surface_root;
+  int n_media;
+  int n_targets;
+  float rem_prob;
+  DevMedium media[RT_MAX_MEDIA];
+  DevTarget targets[RT_MAX_TARGETS];
+  DevCamera cam;
+  uint32_t key0, key1;
+  int n_shards, shard, row_block, tile_rows;
+};
+
+// Host-side scene image, ready for upload (rt_build.cpp).
+struct HostScene {
+  std::vector<float> nodes, prims, prim_uv, motions, uvframes;
+  std::vector<int> prim_mat;
+  std::vector<DevMaterial> mats;
+  std::vector<DevTexture> texs;
+  int surface_root = RT_EMPTY_ROOT;
+  int n_media = 0;
+  DevMedium media[RT_MAX_MEDIA];
+  int n_nodes = 0, n_prims = 0, max_depth = 0;
+};
+
+struct rt_scene;
+struct rt_camera_settings;
+struct rt_exec;
+
+// rt_build.cpp (host only; return RT_OK or RT_E_*, message in err)
+int rt_host_build_scene(const rt_scene* sc, HostScene& out, std::string& err);
+int rt_host_image_height(const rt_camera_settings* cs);
+int rt_host_shard_rows(int height, const rt_exec* ex);
+// fills camera / targets / tiling / key of P (pointers are left to the caller)
+int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex, KernelParams& P,
+                        std::string& err);
+
+// rt_kernel.hip (device launchers)
+int rt_launch_render(const KernelParams& p, void* stream);
+int rt_launch_encode8(const float* in, uint8_t* out, int64_t n, int encoding, void* stream);

@@ -1,0 +1,545 @@
+// rt_trace.h — the per-lane path-tracing logic of the MI355X megakernel (rt_kernel.hip).
+//
+// One lane owns one pixel and loops over its `samples_per_pixel` paths with path
+// regeneration: a lane whose path terminates immediately starts its next sample, so a
+// 64-lane wave keeps tracing until every lane has finished all its samples.  Per segment:
+//   1. closest hit: the surface BVH (stack in LDS, near child first, reference depth-first
+//      tie-break) and, for every constantMedium, its boundary BVH (Geometry.hs:298-330);
+//   2. the material of the hit: a `switch` over the ten reference materials
+//      (Material.hs:41-129) and the texture (Texture.hs:18-53);
+//   3. HemisphereF / SphereF: direction from the redirect mixture, weight pdf1 / pdf
+//      (Ray.hs:187-224).
+// rayColor's recursion (Ray.hs:174-224) is carried as throughput T and radiance L
+// (L = e0 + a0 (e1 + a1 (...)) = sum_k T_k e_k).
+//
+// FP32 arithmetic; Philox4x32-10 keyed by the seed with counter (pixel, sample, segment,
+// event) and 24-bit uniforms; direct samplers in place of the reference's rejection loops
+// (same distributions).  The FP64 oracle's Philox mode (oracle/rt_oracle.c) consumes the same
+// numbers, which is what the per-pixel parity tests check.
+//
+// The header is compiled by hipcc for gfx950 (rt_kernel.hip).  tests/kernel_emu compiles the
+// same text for the host (RT_HOST_EMU) so the kernel's logic can be checked against the oracle
+// without a GPU; that build is test tooling and is never linked into the product library.
+#pragma once
+#include <stdint.h>
+
+#include "rt_internal.h"
+
+#ifdef RT_HOST_EMU
+#include <cmath>
+#include <cstring>
+#define RT_FN static inline
+namespace rt_emu {
+inline uint32_t umulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
+inline int f2i(float f) {
+  int i;
+  std::memcpy(&i, &f, 4);
+  return i;
+}
+}  // namespace rt_emu
+#define RT_UMULHI(a, b) rt_emu::umulhi(a, b)
+#define RT_F2I(f) rt_emu::f2i(f)
+#define RT_SINCOS(x, s, c) (*(s) = sinf(x), *(c) = cosf(x))
+#define RT_LOG(x) logf(x)
+#define RT_RSQRT(x) (1.0f / sqrtf(x))
+#else
+#define RT_FN __device__ __forceinline__
+#define RT_UMULHI(a, b) __umulhi(a, b)
+#define RT_F2I(f) __float_as_int(f)
+#define RT_SINCOS(x, s, c) __sincosf(x, s, c)
+#define RT_LOG(x) __logf(x)
+#define RT_RSQRT(x) __frsqrt_rn(x)
+#endif
+
+namespace rtk {
+
+constexpr float kPi = 3.14159265358979323846f;
+constexpr float kTmin = 0.0001f;  // Ray.hs:178
+constexpr float kInf = __builtin_huge_valf();
+
+struct alignas(16) v4 {
+  float x, y, z, w;
+};
+struct alignas(16) i4 {
+  int x, y, z, w;
+};
+struct alignas(8) v2 {
+  float x, y;
+};
+struct f3 {
+  float x, y, z;
+};
+RT_FN f3 mk3(float x, float y, float z) { return f3{x, y, z}; }
+RT_FN f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
+RT_FN f3 operator+(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+RT_FN f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+RT_FN f3 operator-(f3 a) { return f3{-a.x, -a.y, -a.z}; }
+RT_FN f3 operator*(float s, f3 a) { return f3{s * a.x, s * a.y, s * a.z}; }
+RT_FN f3 operator*(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+RT_FN float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+RT_FN f3 normalize(f3 v) {
+  float l = dot(v, v);
+  if (l <= 1e-12f) return v;  // linear's normalize leaves (near-)zero vectors alone
+  return RT_RSQRT(l) * v;
+}
+RT_FN f3 reflect(f3 n, f3 v) { return v - (2.0f * dot(n, v)) * n; }  // Core.hs:49-51
+RT_FN f3 xyz(v4 v) { return f3{v.x, v.y, v.z}; }
+RT_FN v4 ld4(const float* p) { return *reinterpret_cast<const v4*>(p); }
+
+// ------------------------------------------------------------------ Philox4x32-10
+struct u4 {
+  uint32_t x, y, z, w;
+};
+RT_FN u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    uint32_t hi0 = RT_UMULHI(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    uint32_t hi1 = RT_UMULHI(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+  }
+  return u4{c0, c1, c2, c3};
+}
+// [0, 1) with 24 random bits: exact in both FP32 and the oracle's FP64
+RT_FN float u01(uint32_t w) { return (float)(w >> 8) * (1.0f / 16777216.0f); }
+
+// uniform direction on the unit sphere (the distribution of randomUnitVector, Core.hs:54-60)
+RT_FN f3 unit_vector(uint32_t a, uint32_t b) {
+  float z = 1.0f - 2.0f * u01(a);
+  float r = sqrtf(fmaxf(0.0f, 1.0f - z * z));
+  float s, c;
+  RT_SINCOS(2.0f * kPi * u01(b), &s, &c);
+  return mk3(r * c, r * s, z);
+}
+
+struct RayCtx {
+  f3 o, d, idir, oidir;
+  float time;
+  int self_gid;
+};
+
+RT_FN f3 motion_shift(const KernelParams& P, int m, float time) {
+  f3 v0 = ld3(P.motions + 8 * m), v1 = ld3(P.motions + 8 * m + 4);
+  return (1.0f - time) * v0 + time * v1;
+}
+
+// Closest hit within (tmin, tbest) over one BVH; ties go to the smaller depth-first `order`
+// (the reference's group / bvhNode tie-break).  stack[k * stride] is this lane's stack.
+RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmin, float& tbest, int& best,
+                     int& best_order, int* stack, int stride, int* overflow) {
+  if (root == RT_EMPTY_ROOT) return;
+  int sp = 0;
+  int node = root;
+  for (;;) {
+    if (node >= 0) {
+      const float* nd = P.nodes + 16 * (size_t)node;
+      v4 n0 = ld4(nd), n1 = ld4(nd + 4), n2 = ld4(nd + 8);
+      i4 n3 = *reinterpret_cast<const i4*>(nd + 12);
+      float lx0 = fmaf(n0.x, R.idir.x, -R.oidir.x), lx1 = fmaf(n0.y, R.idir.x, -R.oidir.x);
+      float ly0 = fmaf(n0.z, R.idir.y, -R.oidir.y), ly1 = fmaf(n0.w, R.idir.y, -R.oidir.y);
+      float lz0 = fmaf(n2.x, R.idir.z, -R.oidir.z), lz1 = fmaf(n2.y, R.idir.z, -R.oidir.z);
+      float rx0 = fmaf(n1.x, R.idir.x, -R.oidir.x), rx1 = fmaf(n1.y, R.idir.x, -R.oidir.x);
+      float ry0 = fmaf(n1.z, R.idir.y, -R.oidir.y), ry1 = fmaf(n1.w, R.idir.y, -R.oidir.y);
+      float rz0 = fmaf(n2.z, R.idir.z, -R.oidir.z), rz1 = fmaf(n2.w, R.idir.z, -R.oidir.z);
+      float lnear = fmaxf(fmaxf(fminf(lx0, lx1), fminf(ly0, ly1)), fmaxf(fminf(lz0, lz1), tmin));
+      float lfar = fminf(fminf(fmaxf(lx0, lx1), fmaxf(ly0, ly1)), fminf(fmaxf(lz0, lz1), tbest));
+      float rnear = fmaxf(fmaxf(fminf(rx0, rx1), fminf(ry0, ry1)), fmaxf(fminf(rz0, rz1), tmin));
+      float rfar = fminf(fminf(fmaxf(rx0, rx1), fmaxf(ry0, ry1)), fminf(fmaxf(rz0, rz1), tbest));
+      bool hl = lnear <= lfar, hr = rnear <= rfar;
+      if (hl && hr) {
+        int nearc = n3.x, farc = n3.y;
+        if (rnear < lnear) {
+          nearc = n3.y;
+          farc = n3.x;
+        }
+        if (sp < RT_STACK_DEPTH) {
+          stack[sp * stride] = farc;
+          ++sp;
+        } else {
+          *overflow = 1;
+        }
+        node = nearc;
+        continue;
+      }
+      if (hl) {
+        node = n3.x;
+        continue;
+      }
+      if (hr) {
+        node = n3.y;
+        continue;
+      }
+    } else {
+      int enc = ~node;
+      int first = enc >> 4, count = (enc & 15) + 1;
+      for (int k = 0; k < count; ++k) {
+        int pi = first + k;
+        const float* pr = P.prims + 16 * (size_t)pi;
+        v4 a = ld4(pr), b = ld4(pr + 4);
+        int kf = RT_F2I(a.w);
+        f3 o = R.o;
+        if (kf & RT_FLAG_MOTION) o = o - motion_shift(P, RT_F2I(pr[15]), R.time);
+        int gid = RT_F2I(b.w);
+        float t;
+        if ((kf & RT_KIND_MASK) == 0) {
+          // sphere (Geometry.hs:58-94); geometric discriminant for FP32 robustness
+          f3 oc = xyz(a) - o;
+          float h = dot(R.d, oc);
+          if (gid == R.self_gid) {
+            // origin on this sphere: the roots are 0 and 2h, only the far one is reachable
+            t = 2.0f * h;
+          } else {
+            f3 l = oc - h * R.d;
+            float disc = b.y - dot(l, l);
+            if (!(disc >= 0.0f)) continue;
+            float sq = sqrtf(disc);
+            float r1 = h - sq, r2 = h + sq;
+            t = (r1 > tmin) ? r1 : r2;
+          }
+          if (!(t > tmin && t <= tbest && t < kInf)) continue;
+        } else {
+          // planeShape (Geometry.hs:117-144)
+          if (gid == R.self_gid) continue;
+          f3 n = xyz(a);
+          float denom = dot(n, R.d);
+          if (!(fabsf(denom) > 1e-8f)) continue;
+          f3 qo = xyz(b) - o;
+          t = dot(n, qo) / denom;
+          if (!(t > tmin && t <= tbest && t < kInf)) continue;
+          v4 c = ld4(pr + 8), e = ld4(pr + 12);
+          f3 prel = t * R.d - qo;
+          float aa = dot(prel, xyz(c)), bb = dot(prel, xyz(e));
+          bool inside = ((kf & RT_KIND_MASK) == 1) ? (aa >= 0.0f && aa <= 1.0f && bb >= 0.0f && bb <= 1.0f)
+                                                   : (aa >= 0.0f && bb >= 0.0f && aa + bb <= 1.0f);
+          if (!inside) continue;
+        }
+        int ord = RT_F2I(pr[11]);
+        if (t < tbest || ord < best_order) {
+          tbest = t;
+          best = pi;
+          best_order = ord;
+        }
+      }
+    }
+    if (sp == 0) break;
+    --sp;
+    node = stack[sp * stride];
+  }
+}
+
+struct HitInfo {
+  f3 p, n;
+  bool front;
+  float u, v;
+  int mat;
+  int gid;
+};
+
+// front side of a boundary hit (constantMedium's case split, Geometry.hs:308)
+RT_FN bool prim_front(const KernelParams& P, int pi, const RayCtx& R, float t) {
+  const float* pr = P.prims + 16 * (size_t)pi;
+  v4 a = ld4(pr);
+  int kf = RT_F2I(a.w);
+  if ((kf & RT_KIND_MASK) == 0) {
+    f3 c = xyz(a);
+    if (kf & RT_FLAG_MOTION) c = c + motion_shift(P, RT_F2I(pr[15]), R.time);
+    f3 p = R.o + t * R.d;
+    return dot(R.d, p - c) * (pr[4] < 0.0f ? -1.0f : 1.0f) <= 0.0f;
+  }
+  return dot(xyz(a), R.d) < 0.0f;
+}
+
+RT_FN HitInfo surface_info(const KernelParams& P, int pi, const RayCtx& R, float t) {
+  HitInfo h;
+  const float* pr = P.prims + 16 * (size_t)pi;
+  v4 a = ld4(pr), b = ld4(pr + 4);
+  int kf = RT_F2I(a.w);
+  h.p = R.o + t * R.d;
+  h.gid = RT_F2I(b.w);
+  h.mat = P.prim_mat[pi];
+  if ((kf & RT_KIND_MASK) == 0) {
+    f3 c = xyz(a);
+    if (kf & RT_FLAG_MOTION) c = c + motion_shift(P, RT_F2I(pr[15]), R.time);
+    f3 outward = (1.0f / b.x) * (h.p - c);
+    h.front = dot(R.d, outward) <= 0.0f;
+    h.n = h.front ? outward : -outward;
+    int uvf = RT_F2I(b.z);
+    f3 on = outward;
+    if (uvf >= 0) {
+      const float* fr = P.uvframes + 12 * uvf;
+      on = mk3(dot(ld3(fr), outward), dot(ld3(fr + 4), outward), dot(ld3(fr + 8), outward));
+    }
+    // sphereUV (Geometry.hs:100-104)
+    h.u = atan2f(on.x, on.z) * (0.5f / kPi) + 0.5f;
+    h.v = acosf(fminf(1.0f, fmaxf(-1.0f, -on.y))) * (1.0f / kPi);
+  } else {
+    f3 n = xyz(a);
+    float denom = dot(n, R.d);
+    h.front = denom < 0.0f;
+    h.n = h.front ? n : -n;
+    f3 o = R.o;
+    if (kf & RT_FLAG_MOTION) o = o - motion_shift(P, RT_F2I(pr[15]), R.time);
+    f3 prel = (o + t * R.d) - xyz(b);
+    float aa = dot(prel, ld3(pr + 8)), bb = dot(prel, ld3(pr + 12));
+    const float* uv = P.prim_uv + 6 * (size_t)pi;
+    float w0 = 1.0f - aa - bb;
+    h.u = w0 * uv[0] + aa * uv[2] + bb * uv[4];
+    h.v = w0 * uv[1] + aa * uv[3] + bb * uv[5];
+  }
+  return h;
+}
+
+RT_FN f3 eval_texture(const KernelParams& P, int tex, float u, float v) {
+  const DevTexture& T = P.texs[tex];
+  f3 c0 = ld3(T.c0);
+  if (T.kind == 0) return c0;
+  // checkerTexture (Texture.hs:45-53)
+  int i = (int)floorf(u * (float)T.nu), j = (int)floorf(v * (float)T.nv);
+  return ((i + j) & 1) == 0 ? c0 : ld3(T.c1);
+}
+
+// rt_hit of a redirect target: parallelogram on (0, infinity) (Ray.hs:143-145)
+RT_FN bool target_hit(const DevTarget& T, f3 o, f3 d, float& t) {
+  f3 n = ld3(T.n);
+  float denom = dot(n, d);
+  if (!(fabsf(denom) > 1e-8f)) return false;
+  f3 qo = ld3(T.q) - o;
+  t = dot(n, qo) / denom;
+  if (!(t > 0.0f)) return false;
+  f3 prel = t * d - qo;
+  float a = dot(prel, ld3(T.wa)), b = dot(prel, ld3(T.wb));
+  return a >= 0.0f && a <= 1.0f && b >= 0.0f && b <= 1.0f;
+}
+
+// All samples of one tile pixel; writes the mean colour.  Returns the stack-overflow flag.
+RT_FN int render_pixel(const KernelParams& P, int tile_pixel, int* stack, int stride) {
+  int overflow = 0;
+  const int W = P.cam.width;
+  const int tr = tile_pixel / W, px = tile_pixel - tr * W;
+  const int gy = ((tr / P.row_block) * P.n_shards + P.shard) * P.row_block + (tr % P.row_block);
+  float* out = P.out + 3 * (size_t)tile_pixel;
+  if (gy >= P.cam.height) {  // padding row of the shard
+    out[0] = 0.0f;
+    out[1] = 0.0f;
+    out[2] = 0.0f;
+    return 0;
+  }
+  const uint32_t pix = (uint32_t)(gy * W + px);
+  const int spp = P.cam.spp, max_depth = P.cam.max_depth;
+  const f3 center = ld3(P.cam.center), top_left = ld3(P.cam.top_left), pu = ld3(P.cam.pixel_u),
+           pv = ld3(P.cam.pixel_v), du = ld3(P.cam.disk_u), dv = ld3(P.cam.disk_v);
+
+  f3 acc = mk3(0.f, 0.f, 0.f);
+  f3 L = acc, T = mk3(1.f, 1.f, 1.f);
+  RayCtx R;
+  R.o = R.d = R.idir = R.oidir = acc;
+  R.time = 0.0f;
+  R.self_gid = -1;
+  int sample = 0, seg = 0;
+  bool alive = false;
+  for (;;) {
+    if (!alive) {
+      if (sample >= spp || max_depth <= 0) break;
+      // Ray.hs:157-172, 229: time, defocus-disk point, pixel jitter
+      u4 w0 = philox(pix, (uint32_t)sample, 0u, RT_EV_CAMERA0, P.key0, P.key1);
+      u4 w1 = philox(pix, (uint32_t)sample, 0u, RT_EV_CAMERA1, P.key0, P.key1);
+      R.time = u01(w0.x);
+      float rad = sqrtf(u01(w0.y)), s, c;
+      RT_SINCOS(2.0f * kPi * u01(w0.z), &s, &c);
+      f3 origin = center + (rad * c) * du + (rad * s) * dv;
+      f3 target = top_left + ((float)px + u01(w0.w)) * pu + ((float)gy + u01(w1.x)) * pv;
+      R.o = origin;
+      R.d = normalize(target - origin);
+      R.self_gid = -1;
+      L = mk3(0.f, 0.f, 0.f);
+      T = mk3(1.f, 1.f, 1.f);
+      seg = 0;
+      alive = true;
+    }
+    // ---- closest hit over the surfaces and every medium (Ray.hs:178)
+    R.idir = mk3(1.0f / (fabsf(R.d.x) > 1e-20f ? R.d.x : copysignf(1e-20f, R.d.x)),
+                 1.0f / (fabsf(R.d.y) > 1e-20f ? R.d.y : copysignf(1e-20f, R.d.y)),
+                 1.0f / (fabsf(R.d.z) > 1e-20f ? R.d.z : copysignf(1e-20f, R.d.z)));
+    R.oidir = R.o * R.idir;
+    float tbest = kInf;
+    int best = -1, best_order = 0x7fffffff;
+    trace_set(P, P.surface_root, R, kTmin, tbest, best, best_order, stack, stride, &overflow);
+    int hit_medium = -1;
+    for (int m = 0; m < P.n_media; ++m) {
+      // constantMedium (Geometry.hs:306-328)
+      const DevMedium& M = P.media[m];
+      float t1 = kInf;
+      int b1 = -1, o1 = 0x7fffffff;
+      trace_set(P, M.root, R, kTmin, t1, b1, o1, stack, stride, &overflow);
+      if (b1 < 0) continue;
+      float lo, hi;
+      if (prim_front(P, b1, R, t1)) {
+        if (!(t1 < tbest)) continue;
+        float t2 = kInf;
+        int b2 = -1, o2 = 0x7fffffff;
+        trace_set(P, M.root, R, t1, t2, b2, o2, stack, stride, &overflow);
+        if (b2 < 0) continue;
+        lo = t1;
+        hi = t2;
+      } else {
+        lo = kTmin;
+        hi = t1;
+      }
+      u4 wm = philox(pix, (uint32_t)sample, (uint32_t)seg, RT_EV_MEDIA + (uint32_t)(m >> 2), P.key0, P.key1);
+      uint32_t wsel = (m & 3) == 0 ? wm.x : (m & 3) == 1 ? wm.y : (m & 3) == 2 ? wm.z : wm.w;
+      float rnd = 1.0f - u01(wsel);
+      float hit_dist = M.neg_inv_density * RT_LOG(rnd);
+      if (hit_dist < hi - lo) {
+        float t = lo + hit_dist;
+        if (t < tbest) {
+          tbest = t;
+          hit_medium = m;
+        }
+      }
+    }
+    bool terminate = false;
+    if (hit_medium < 0 && best < 0) {
+      // miss: cs_background (Ray.hs:179)
+      f3 bg = ld3(P.cam.bg0);
+      if (P.cam.bg_kind == 1) {
+        float a = 0.5f * (R.d.y + 1.0f);
+        bg = (1.0f - a) * bg + a * ld3(P.cam.bg1);
+      }
+      L = L + T * bg;
+      terminate = true;
+    } else {
+      HitInfo h;
+      if (hit_medium >= 0) {
+        h.p = R.o + tbest * R.d;
+        h.n = -R.d;
+        h.front = true;
+        h.u = 0.f;
+        h.v = 0.f;
+        h.mat = P.media[hit_medium].material;
+        h.gid = -1;
+      } else {
+        h = surface_info(P, best, R, tbest);
+      }
+      const DevMaterial& Mt = P.mats[h.mat];
+      u4 w = philox(pix, (uint32_t)sample, (uint32_t)seg, RT_EV_SCATTER, P.key0, P.key1);
+      const bool last = seg + 1 >= max_depth;  // rayColor (depth - 1) with depth - 1 <= 0 is zero
+      f3 newdir = R.d;
+      switch (Mt.kind) {
+        case 0:  // lightSource: emit, Absorb
+          L = L + T * eval_texture(P, Mt.tex, h.u, h.v);
+          terminate = true;
+          break;
+        case 1:  // pitchBlack
+          terminate = true;
+          break;
+        case 4:  // mirror
+          T = T * eval_texture(P, Mt.tex, h.u, h.v);
+          newdir = reflect(h.n, R.d);
+          break;
+        case 5: {  // metal
+          f3 d2 = reflect(h.n, R.d) + Mt.param * unit_vector(w.y, w.z);
+          if (dot(d2, h.n) > 0.0f) {
+            T = T * eval_texture(P, Mt.tex, h.u, h.v);
+            newdir = normalize(d2);
+          } else {
+            terminate = true;
+          }
+          break;
+        }
+        case 6: {  // dielectric
+          float ior = Mt.param;
+          float ratio = h.front ? 1.0f / ior : ior;
+          float cos_t = fminf(1.0f, -dot(h.n, R.d));
+          float sin_t = sqrtf(fmaxf(0.0f, 1.0f - cos_t * cos_t));
+          float r0 = (1.0f - ratio) / (1.0f + ratio);
+          r0 = r0 * r0;
+          float x1 = 1.0f - cos_t, x2 = x1 * x1;
+          float reflectance = r0 + (1.0f - r0) * (x2 * x2 * x1);
+          if (ratio * sin_t > 1.0f || u01(w.x) < reflectance) {
+            newdir = reflect(h.n, R.d);
+          } else {
+            f3 perp = ratio * (R.d + cos_t * h.n);
+            newdir = perp - sqrtf(fabsf(1.0f - dot(perp, perp))) * h.n;
+          }
+          break;
+        }
+        case 7:  // transparent
+          T = T * eval_texture(P, Mt.tex, h.u, h.v);
+          break;
+        default: {  // 2 lambertian, 3 lommelSeeliger (HemisphereF); 8 isotropic, 9 anisotropic (SphereF)
+          const bool hemi = Mt.kind == 2 || Mt.kind == 3;
+          float cr = u01(w.x);
+          int choice = -1;
+          for (int k = 0; k < P.n_targets; ++k) {
+            if (cr < P.targets[k].thresh) {
+              choice = k;
+              break;
+            }
+          }
+          f3 dir;
+          if (choice < 0) {
+            f3 uu = unit_vector(w.y, w.z);
+            dir = hemi ? normalize(h.n + uu) : uu;
+          } else {
+            const DevTarget& Tg = P.targets[choice];
+            f3 lp = ld3(Tg.q) + u01(w.y) * ld3(Tg.u) + u01(w.z) * ld3(Tg.v);
+            dir = normalize(lp - h.p);
+          }
+          float pdf1 = hemi ? dot(dir, h.n) * (1.0f / kPi) : 0.25f / kPi;
+          if (hemi && pdf1 <= 0.0f) {
+            terminate = true;
+            break;
+          }
+          float mix = 0.0f;
+          for (int k = 0; k < P.n_targets; ++k) {
+            float tt;
+            if (target_hit(P.targets[k], h.p, dir, tt))
+              mix += P.targets[k].prob * (tt * tt / fabsf(dot(ld3(P.targets[k].cr), dir)));
+          }
+          float pdf = P.rem_prob * pdf1 + mix;
+          f3 f = eval_texture(P, Mt.tex, h.u, h.v);
+          if (Mt.kind == 3) {
+            float mu0 = -dot(R.d, h.n), mu1 = dot(dir, h.n);
+            f = (0.25f / (mu0 + mu1)) * f;
+          } else if (Mt.kind == 9) {
+            float g = Mt.param, mu = dot(R.d, dir);
+            float base = 1.0f + g * g - 2.0f * g * mu;
+            f = ((1.0f - g * g) / (base * sqrtf(base))) * f;
+          }
+          T = T * ((pdf1 / pdf) * f);
+          newdir = dir;
+          break;
+        }
+      }
+      if (!terminate) {
+        if (last) {
+          terminate = true;
+        } else {
+          R.o = h.p;
+          R.d = newdir;
+          R.self_gid = h.gid;
+          ++seg;
+        }
+      }
+    }
+    if (terminate) {
+      acc = acc + L;
+      alive = false;
+      ++sample;
+    }
+  }
+  const float inv = 1.0f / (float)spp;
+  out[0] = acc.x * inv;
+  out[1] = acc.y * inv;
+  out[2] = acc.z * inv;
+  return overflow;
+}
+
+}  // namespace rtk

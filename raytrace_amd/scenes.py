@@ -1,0 +1,180 @@
+"""The benchmark / parity scenes (BASELINE.json configs), built with the mirrored constructors
+exactly as the reference writes them.  Each returns (CameraSettings, world, StdGen).
+
+  readme_scene   README.md:41-55 (config 1, `example_image.png`)
+  cornell_box    test/Main.hs:188-218 (config 2, `cornell_box_redirect.png`)
+  demo1          test/Main.hs:136-186 (config 3; the reference seeds it with newStdGen,
+                 here a fixed mkStdGen so the world is reproducible)
+  bunny_cornell  config 4 (composed: Cornell walls + light + images/bunny.obj)
+  pawn_fog       config 5 (composed: pawnTest, test/Main.hs:323-344, plus a fog sphere)
+  pawn_test      test/Main.hs:323-344 verbatim (`pawn_demo.png`)
+"""
+from __future__ import annotations
+
+import os
+
+from .camera import constBackground, defaultCameraSettings, grayFade, sky
+from .core import V3, degrees, mkStdGen, midpoint, norm, sub
+from .geometry import (boundingBox, bvhTree, cuboid, constantMedium, group, parallelogram, pureGeometry, readObj,
+                       rotateY, scale, sphere, transform, transformVertices, translate, triangleMesh)
+from .material import (checkerTexture, constantTexture, dielectric, isotropic, lambertian, lightSource, metal,
+                       mirror)
+from .core import fromCorners
+
+DATA_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data")
+
+
+def readme_scene(width=600, spp=50):
+    world = group([
+        lambertian(checkerTexture(20, 10, 0.2, 0.8)) << sphere(V3(0, 0, 0), 1),
+        lambertian(constantTexture(V3(0, 0.2, 0.5))) << sphere(V3(0, -1000, 0), 999),
+        mirror(constantTexture(0.8)) << parallelogram(V3(-3.25, -1, -0.75), V3(1.25, 0, -1.25), V3(0, 2, 0)),
+    ])
+    settings = defaultCameraSettings(cs_center=V3(-0.75, 0, 2), cs_lookAt=V3(0, 0, -1), cs_aspectRatio=16 / 9,
+                                     cs_imageWidth=width, cs_samplesPerPixel=spp)
+    return settings, world, mkStdGen(100)
+
+
+def cornell_walls(light_emit=15.0):
+    red = lambertian(constantTexture(V3(0.65, 0.05, 0.05)))
+    white = lambertian(constantTexture(V3(0.73, 0.73, 0.73)))
+    green = lambertian(constantTexture(V3(0.12, 0.45, 0.15)))
+    light = lightSource(constantTexture(V3(light_emit, light_emit, light_emit)))
+    return [
+        green << parallelogram(V3(555, 0, 0), V3(0, 555, 0), V3(0, 0, 555)),
+        red << parallelogram(V3(0, 0, 0), V3(0, 555, 0), V3(0, 0, 555)),
+        light << parallelogram(V3(343, 554, 332), V3(-130, 0, 0), V3(0, 0, -105)),
+        white << parallelogram(V3(0, 0, 0), V3(555, 0, 0), V3(0, 0, 555)),
+        white << parallelogram(V3(555, 555, 555), V3(-555, 0, 0), V3(0, 0, -555)),
+        white << parallelogram(V3(0, 0, 555), V3(555, 0, 0), V3(0, 555, 0)),
+    ], white
+
+
+CORNELL_TARGETS = [(0.25, V3(343, 554, 332), V3(-130, 0, 0), V3(0, 0, -105))]
+
+
+def cornell_settings(width=600, spp=200, depth=50, redirect=True):
+    return defaultCameraSettings(
+        cs_aspectRatio=1.0, cs_imageWidth=width, cs_samplesPerPixel=spp, cs_maxRecursionDepth=depth,
+        cs_background=constBackground(V3(0, 0, 0)), cs_vfov=degrees(40), cs_center=V3(278, 278, -800),
+        cs_lookAt=V3(278, 278, 0), cs_redirectTargets=list(CORNELL_TARGETS) if redirect else [])
+
+
+def cornell_box(spp=200, depth=50, width=600, redirect=True):
+    walls, white = cornell_walls()
+    world = group(walls + [
+        transform(translate(V3(265, 0, 295)) @ rotateY(degrees(15)),
+                  white << cuboid(fromCorners(V3(0, 0, 0), V3(165, 330, 165)))),
+        transform(translate(V3(130, 0, 65)) @ rotateY(degrees(-18)),
+                  white << cuboid(fromCorners(V3(0, 0, 0), V3(165, 165, 165)))),
+    ])
+    return cornell_settings(width, spp, depth, redirect), world, mkStdGen(234)
+
+
+def demo1_world(gen):
+    """genWorld of test/Main.hs:150-168 evaluated with the splitmix StdGen; returns (world, gen')."""
+    material_ground = lambertian(constantTexture(V3(0.5, 0.5, 0.5)))
+    material_glass = dielectric(1.5)
+    material_diffuse = lambertian(constantTexture(V3(0.4, 0.2, 0.1)))
+    material_mirror = mirror(constantTexture(V3(0.7, 0.6, 0.5)))
+    big = [
+        material_ground << sphere(V3(0, -1000, 0), 1000),
+        material_glass << sphere(V3(0, 1, 0), 1),
+        material_diffuse << sphere(V3(-4, 1, 0), 1),
+        material_mirror << sphere(V3(4, 1, 0), 1),
+    ]
+    small = []
+    for a in range(-11, 11):
+        for b in range(-11, 11):
+            ox, gen = gen.randomR(0.0, 0.9)
+            oz, gen = gen.randomR(0.0, 0.9)
+            center = (float(a) + ox, 0.2, float(b) + oz)
+            if norm(sub(center, V3(4, 0.2, 0))) <= 0.9:
+                continue
+            choose, gen = gen.random()
+            if choose < 0.8:
+                c1 = []
+                for _ in range(3):
+                    x, gen = gen.random()
+                    c1.append(x)
+                c2 = []
+                for _ in range(3):
+                    x, gen = gen.random()
+                    c2.append(x)
+                mat = lambertian(constantTexture(V3(c1[0] * c2[0], c1[1] * c2[1], c1[2] * c2[2])))
+            elif choose < 0.95:
+                fuzz, gen = gen.randomR(0.0, 0.5)
+                col = []
+                for _ in range(3):
+                    x, gen = gen.randomR(0.5, 1.0)
+                    col.append(x)
+                mat = metal(fuzz, constantTexture(V3(*col)))
+            else:
+                mat = material_glass
+            small.append(mat << sphere(center, 0.2))
+    return bvhTree(big + small), gen
+
+
+def demo1(width=1200, spp=500, depth=50, seed=1):
+    world, gen2 = demo1_world(mkStdGen(seed))
+    settings = defaultCameraSettings(
+        cs_aspectRatio=16 / 9, cs_imageWidth=width, cs_samplesPerPixel=spp, cs_maxRecursionDepth=depth,
+        cs_vfov=degrees(20), cs_center=V3(13, 2, 3), cs_lookAt=V3(0, 0, 0), cs_defocusAngle=degrees(0.6),
+        cs_focusDist=10, cs_background=sky)
+    return settings, world, gen2
+
+
+def load_mesh(name):
+    return readObj(os.path.join(DATA_DIR, name))
+
+
+def bunny_cornell(width=800, spp=1000, depth=50):
+    """Config 4 (composed, documented in DESIGN.md): the Cornell walls and light of config 2
+    with images/bunny.obj centred on its bbox midpoint (as bunnyTest, test/Main.hs:376),
+    rotated 30 degrees about y, scaled by 2000 and set on the floor at x = z = 278."""
+    mesh = load_mesh("bunny.obj")
+    center = tuple(midpoint(i) for i in boundingBox(triangleMesh(mesh)))
+    m = rotateY(degrees(30)) @ scale(2000) @ translate(tuple(-c for c in center))
+    m1 = transformVertices(m, mesh)
+    ymin = min(v[1] for v in m1.vertices)
+    mesh2 = transformVertices(translate(V3(278, -ymin, 278)), m1)
+    walls, white = cornell_walls()
+    world = group(walls + [white << triangleMesh(mesh2)])
+    return cornell_settings(width, spp, depth, True), world, mkStdGen(234)
+
+
+def _pawn_world(mesh, fog):
+    pawn = triangleMesh(mesh)
+    objs = [pureGeometry(dielectric(1.5) << pawn),
+            isotropic(constantTexture(V3(1, 0, 0))) << constantMedium(5, pawn)]
+    if fog:
+        objs.append(isotropic(constantTexture(1)) << constantMedium(0.02, sphere(V3(0, 2.75, 0), 20)))
+    return group(objs)
+
+
+def pawn_test(width=500, spp=400, depth=20):
+    mesh = transformVertices(scale(100), load_mesh("pawn.obj"))
+    settings = defaultCameraSettings(cs_center=V3(0, 3.75, 5), cs_lookAt=V3(0, 2.75, 0), cs_imageWidth=width,
+                                     cs_vfov=degrees(80), cs_samplesPerPixel=spp, cs_maxRecursionDepth=depth,
+                                     cs_background=grayFade)
+    return settings, _pawn_world(mesh, fog=False), mkStdGen(55)
+
+
+def pawn_fog(width=800, spp=2000, depth=20):
+    """Config 5 (composed): pawnTest plus an isotropic fog sphere (density 0.02, radius 20)
+    enclosing the camera, which exercises the ray-starts-inside case (Geometry.hs:313)."""
+    mesh = transformVertices(scale(100), load_mesh("pawn.obj"))
+    settings = defaultCameraSettings(cs_center=V3(0, 3.75, 5), cs_lookAt=V3(0, 2.75, 0), cs_imageWidth=width,
+                                     cs_vfov=degrees(80), cs_samplesPerPixel=spp, cs_maxRecursionDepth=depth,
+                                     cs_background=grayFade)
+    return settings, _pawn_world(mesh, fog=True), mkStdGen(55)
+
+
+CONFIGS = {
+    "readme": readme_scene,
+    "cornell": cornell_box,
+    "demo1": demo1,
+    "bunny_cornell": bunny_cornell,
+    "pawn_fog": pawn_fog,
+    "pawn_test": pawn_test,
+}

@@ -1,0 +1,45 @@
+"""ctypes front-end of the host emulator of the kernel logic (TEST TOOLING)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "librt_emu.so")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-C", HERE, "-s"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        _lib = ctypes.CDLL(LIB)
+        _lib.rt_emu_last_error.restype = ctypes.c_char_p
+    return _lib
+
+
+def render(settings, world, seed, n_shards=1, shard=0, row_block=4, nthreads=None):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from raytrace_amd import _lib as R
+    from raytrace_amd.camera import image_height
+    from raytrace_amd.ray import _seed64, shard_rows
+    from raytrace_amd.scene import FlatScene, flatten
+    flat = world if isinstance(world, FlatScene) else flatten(world)
+    cs = R.camera_struct(settings)
+    sc = R.scene_struct(flat)
+    ex = R.exec_struct(0, n_shards, shard, row_block)
+    h = image_height(settings)
+    rows = shard_rows(h, n_shards, row_block)
+    out = np.zeros((rows, int(settings.cs_imageWidth), 3), np.float32)
+    L = lib()
+    rc = L.rt_emu_render(ctypes.byref(cs), ctypes.byref(sc), ctypes.c_uint64(_seed64(seed)), ctypes.byref(ex),
+                         out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(nthreads or min(16, os.cpu_count() or 1)))
+    if rc != 0:
+        raise RuntimeError(f"rt_emu_render failed {rc}: {L.rt_emu_last_error().decode()}")
+    return out
