@@ -1,0 +1,195 @@
+"""Benchmark of the MI355X path-tracing kernel on BASELINE.json's headline config.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cornell]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = one full frame of the config (Cornell box 600x600, 200 spp, depth 50, redirect
+target, seed 234 — test/Main.hs:188-218) with the scene already resident in HBM.  With N
+ranks (one process per GPU) the frame's rows are dealt to ranks in blocks of 4
+(rt_exec row interleave) and the framebuffer tiles are gathered over RCCL (all_gather into one
+tensor) inside the timed step; `value` = pixels x spp of all ranks / max-over-ranks time.
+
+Extra fields: `roofline` (the render kernel's SURVEY.md §8(d) algorithmic bytes per launch /
+its HIP-event-timed duration vs the 8 TB/s HBM peak; `traffic` = PMC-measured HBM bytes per
+launch from the committed rocprofv3 summary, when present) and `cpu_baseline` (the FP64
+oracle, the CPU restatement of the reference's algorithm, on a bounded row sample, rank 0 at
+N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
+PUBLISHED_MSAMPLES = {"cornell": 1.2}  # Cornell 600x600x200 with redirect ~1:00 (author's laptop)
+METRIC = "Msamples/s (pixels×spp/s) + achieved HBM GB/s, Cornell-box 600×600"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(config, world_fn, row_stride=6):
+    """Time the oracle (binary64 restatement, splitmix draw order) on every `row_stride`-th row."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle
+    from raytrace_amd.camera import image_height
+    cs, world, seed = world_fn()
+    h, w = image_height(cs), cs.cs_imageWidth
+    rows = np.arange(0, h, row_stride)
+    pix = (rows[:, None] * w + np.arange(w)[None, :]).reshape(-1).astype(np.int32)
+    threads = min(16, os.cpu_count() or 1)
+    oracle.render(cs, world, seed, mode=oracle.RNG_SPLITMIX, pixels=pix[:64], nthreads=threads)  # warm
+    t0 = time.perf_counter()
+    oracle.render(cs, world, seed, mode=oracle.RNG_SPLITMIX, pixels=pix, nthreads=threads)
+    dt = time.perf_counter() - t0
+    samples = len(pix) * cs.cs_samplesPerPixel
+    return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"{config}: every {row_stride}th row ({len(rows)} rows x {w} px x {cs.cs_samplesPerPixel} spp"
+                      f" = {samples / 1e6:.1f} M samples) in {dt:.2f} s, oracle/rt_oracle.c splitmix mode, "
+                      f"{threads} threads"}
+
+
+def pmc_traffic(config):
+    """HBM bytes per launch of the render kernel from the committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(config, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="cornell", choices=["cornell", "readme", "demo1", "bunny_cornell", "pawn_fog"])
+    ap.add_argument("--row-block", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", action="store_true", help="gather + assemble + sanity-check the frame after timing")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from raytrace_amd import scenes
+    from raytrace_amd.camera import image_height
+    from raytrace_amd.ray import DeviceScene, assemble_shards, shard_rows
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world_size}; using WORLD_SIZE")
+    n = world_size
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if n > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    fn = scenes.CONFIGS[args.config]
+    cs, world, seed = fn()
+    h, w, spp = image_height(cs), cs.cs_imageWidth, cs.cs_samplesPerPixel
+    scene = DeviceScene(world, device=local_rank)
+    rows = shard_rows(h, n, args.row_block)
+    tile = torch.empty((rows, w, 3), dtype=torch.float32, device=dev)
+    gathered = torch.empty((n * rows, w, 3), dtype=torch.float32, device=dev) if n > 1 else None
+    stream = torch.cuda.current_stream(dev)
+
+    ev = []
+
+    def step(timed):
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        scene.render_async(cs, seed, tile.data_ptr(), stream.cuda_stream, n_shards=n, shard=rank,
+                           row_block=args.row_block)
+        if timed:
+            e1.record(stream)
+            ev.append((e0, e1))
+        if n > 1:
+            dist.all_gather_into_tensor(gathered, tile)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    if n > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    if n > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if n > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
+
+    check = None
+    if args.check or rank == 0:
+        import numpy as np
+        if n > 1:
+            tiles = gathered.view(n, rows, w, 3).cpu().numpy()
+            img = assemble_shards(tiles, h, args.row_block)
+        else:
+            img = tile[:h].cpu().numpy()
+        check = {"finite": bool(np.isfinite(img).all()), "mean_rgb": [round(float(x), 5) for x in img.reshape(-1, 3).mean(0)]}
+
+    total_samples = h * w * spp
+    value = total_samples * args.steps / elapsed / 1e6
+    if rank == 0:
+        with open(os.path.join(ROOT, "tests", "golden", "algbytes.json")) as f:
+            alg = json.load(f)["configs"][args.config]
+        b_sample = alg["bytes_per_sample"]
+        from raytrace_amd.ray import shard_row_index
+        real_rows = int((shard_row_index(h, n, rank, args.row_block) < h).sum())
+        samples_per_launch = real_rows * w * spp
+        achieved = b_sample * samples_per_launch / (kernel_ms / 1e3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.config),
+                    "kernel": "rt_render_kernel", "kernel_ms": round(kernel_ms, 4),
+                    "bytes_per_sample": round(b_sample, 1), "samples_per_launch": samples_per_launch}
+        cpu = None
+        if n == 1 and not args.no_cpu_baseline:
+            try:
+                cpu = cpu_baseline(args.config, fn)
+            except Exception as e:  # the baseline must never break the bench line
+                cpu = {"error": repr(e)}
+        pub = PUBLISHED_MSAMPLES.get(args.config)
+        line = {
+            "metric": METRIC if args.config == "cornell" else f"Msamples/s, {args.config}",
+            "value": round(value, 2), "unit": "Msamples/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": round(value / pub, 1) if pub else None, "dtype": "f32",
+            "data": "synthetic (reference scene built in-process, no external data)",
+            "config": {"workload": f"{args.config} {w}x{h} {spp}spp depth {cs.cs_maxRecursionDepth}",
+                       "width": w, "height": h, "spp": spp, "max_depth": cs.cs_maxRecursionDepth,
+                       "parallelism": f"rows interleaved over {n} GPU(s), row_block {args.row_block}"
+                                      + (", RCCL all_gather of the framebuffer" if n > 1 else "")},
+            "roofline": roofline, "cpu_baseline": cpu, "check": check,
+        }
+        print(json.dumps(line), flush=True)
+    if n > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    scene.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -147,8 +147,9 @@ typedef struct rt_camera_settings {
 } rt_camera_settings;
 
 /* Which rows this call renders.  Rows are dealt to shards in blocks of `row_block`
- * round-robin: shard r owns global rows y with (y / row_block) % n_shards == r.  Every shard
- * has the same padded row count (rt_shard_rows); padding rows are written as zeros. */
+ * round-robin: shard r owns global rows y with (y / row_block) % n_shards == r.  With
+ * n_shards > 1 every shard has the same padded row count (rt_shard_rows); padding rows are
+ * written as zeros.  With n_shards == 1 the tile is exactly the image (height rows). */
 typedef struct rt_exec {
   int32_t device;       /* HIP device ordinal */
   int32_t n_shards;     /* >= 1 */

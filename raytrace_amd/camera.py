@@ -77,6 +77,9 @@ def background_of(cs: CameraSettings) -> Background:
 
 def image_height(cs: CameraSettings) -> int:
     """`round (fromIntegral cs_imageWidth / cs_aspectRatio)` with banker's rounding."""
+    if not (cs.cs_aspectRatio > 0) or not math.isfinite(cs.cs_aspectRatio):
+        from .errors import RtInvalid
+        raise RtInvalid(f"aspect ratio {cs.cs_aspectRatio} must be positive and finite")
     return int(round(float(cs.cs_imageWidth) / cs.cs_aspectRatio))
 
 

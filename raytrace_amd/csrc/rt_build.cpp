@@ -71,6 +71,7 @@ int rt_host_image_height(const rt_camera_settings* cs) {
 int rt_host_shard_rows(int height, const rt_exec* ex) {
   if (!ex || ex->n_shards < 1 || ex->row_block < 1 || ex->shard < 0 || ex->shard >= ex->n_shards || height < 0)
     return RT_E_INVALID;
+  if (ex->n_shards == 1) return height;  // the whole image, unpadded
   int blocks = (height + ex->row_block - 1) / ex->row_block;
   int per = (blocks + ex->n_shards - 1) / ex->n_shards;
   return per * ex->row_block;

@@ -1,0 +1,80 @@
+"""Multi-GPU rendering: one process per GPU, rows dealt to ranks, framebuffer gathered over RCCL.
+
+Pixels are independent (Ray.hs:238) and the Philox stream is keyed by the GLOBAL pixel index,
+so any row partition renders exactly the image a single GPU renders.  Rank r owns the rows
+{y : (y / row_block) % world_size == r} (interleaved blocks balance the uneven per-row cost of
+a scene); every rank's tile has the same padded row count, so the exchange is a single
+all_gather_into_tensor of equal-size tiles (0.9 MB per rank at 600x600 on 8 GPUs) — the only
+collective on the path.  Rank 0 un-permutes the rows.
+
+`tile_fn` lets the CPU tests drive the same partition / gather / assembly logic over `gloo`
+with a host renderer; the product path renders on the local GPU through DeviceScene.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .camera import CameraSettings, image_height
+from .ray import DeviceScene, assemble_shards, shard_rows
+
+
+class ShardedRenderer:
+    def __init__(self, settings: CameraSettings, world, row_block: int = 4, device=None, tile_fn=None, group=None):
+        import torch
+        import torch.distributed as dist
+        self.torch = torch
+        self.dist = dist
+        self.group = group
+        self.settings = settings
+        self.row_block = row_block
+        self.world_size = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.h = image_height(settings)
+        self.w = int(settings.cs_imageWidth)
+        self.rows = shard_rows(self.h, self.world_size, row_block)
+        self.tile_fn = tile_fn
+        if tile_fn is None:
+            self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+            self.scene = DeviceScene(world, device=self.device.index or 0)
+        else:
+            self.device = torch.device("cpu")
+            self.scene = None
+            self.world = world
+        self.tile = torch.empty((self.rows, self.w, 3), dtype=torch.float32, device=self.device)
+        self.gathered = torch.empty((self.world_size * self.rows, self.w, 3), dtype=torch.float32, device=self.device)
+
+    def render_tile(self, seed, stream=None):
+        """Enqueue (GPU) or compute (tile_fn) this rank's rows into self.tile."""
+        if self.tile_fn is not None:
+            self.tile.copy_(self.torch.from_numpy(np.ascontiguousarray(
+                self.tile_fn(self.settings, self.world, seed, self.world_size, self.rank, self.row_block))))
+            return
+        s = stream if stream is not None else self.torch.cuda.current_stream(self.device)
+        self.scene.render_async(self.settings, seed, self.tile.data_ptr(), s.cuda_stream, n_shards=self.world_size,
+                                shard=self.rank, row_block=self.row_block)
+
+    def gather(self):
+        if self.world_size > 1:
+            self.dist.all_gather_into_tensor(self.gathered, self.tile, group=self.group)
+        else:
+            self.gathered.copy_(self.tile)
+
+    def step(self, seed, stream=None):
+        self.render_tile(seed, stream)
+        self.gather()
+
+    def image(self) -> np.ndarray:
+        """The assembled (height, width, 3) image (valid on every rank after gather())."""
+        tiles = self.gathered.view(self.world_size, self.rows, self.w, 3).cpu().numpy()
+        return assemble_shards(tiles, self.h, self.row_block)
+
+    def render(self, seed) -> np.ndarray:
+        self.step(seed)
+        if self.tile_fn is None:
+            self.torch.cuda.synchronize(self.device)
+        return self.image()
+
+    def close(self):
+        if self.scene is not None:
+            self.scene.close()
+            self.scene = None

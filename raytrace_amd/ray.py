@@ -42,6 +42,9 @@ def raytrace(settings: CameraSettings, world, seed, device: int = 0, stats: dict
     if h <= 0 or w <= 0:
         from .errors import RtInvalid
         raise RtInvalid(f"image size {w}x{h} must be positive")
+    rows = _lib.check(L.rt_shard_rows(h, ctypes.byref(ex)))
+    if rows != h:
+        raise RuntimeError(f"librt_amd.so reports {rows} rows for a {h}-row image")
     out = np.zeros((h, w, 3), np.float32)
     st = _lib.RtStats()
     _lib.check(L.rt_render(ctypes.byref(cs), ctypes.byref(sc), _seed64(seed), ctypes.byref(ex),
@@ -69,7 +72,9 @@ def render_shard(settings: CameraSettings, world, seed, n_shards: int, shard: in
 
 
 def shard_rows(height: int, n_shards: int, row_block: int) -> int:
-    """Padded rows per shard (pure arithmetic, mirrors rt_shard_rows)."""
+    """Padded rows per shard (pure arithmetic, mirrors rt_shard_rows); a single shard is the image."""
+    if n_shards == 1:
+        return height
     blocks = (height + row_block - 1) // row_block
     return ((blocks + n_shards - 1) // n_shards) * row_block
 

@@ -1,0 +1,123 @@
+"""The C-ABI boundary: librt_amd.so loads without a GPU, exports every function include/rt.h
+declares, and the record layouts the Python mirror writes match the header's C layout."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import numpy as np
+
+from conftest import ROOT
+from raytrace_amd import _lib
+from raytrace_amd import scene as S
+
+HEADER = os.path.join(ROOT, "include", "rt.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(rt_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.load()
+    names = declared_functions()
+    assert len(names) >= 10
+    for n in names:
+        assert hasattr(L, n), n
+    assert set(names) == set(_lib.EXPORTED)
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+    exported = set(re.findall(r"\bT (rt_\w+)", out.stdout))
+    assert set(names) <= exported
+    assert L.rt_abi_version() == 1
+
+
+def test_host_only_entry_points_without_gpu():
+    L = _lib.load()
+    from raytrace_amd import scenes
+    cs = _lib.camera_struct(scenes.readme_scene()[0])
+    assert L.rt_image_height(ctypes.byref(cs)) == 338
+    ex = _lib.exec_struct(n_shards=3, shard=1, row_block=4)
+    assert L.rt_shard_rows(338, ctypes.byref(ex)) == 116       # ceil(ceil(338/4)/3)*4
+    assert L.rt_shard_row(0, ctypes.byref(ex)) == 4 and L.rt_shard_row(5, ctypes.byref(ex)) == 17
+    bad = _lib.exec_struct(n_shards=2, shard=2)
+    assert L.rt_shard_rows(100, ctypes.byref(bad)) == _lib.RT_E_INVALID
+    assert b"invalid" in L.rt_last_error()
+
+
+C_LAYOUT = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "rt.h"
+#define P(T) printf(#T " %zu\n", sizeof(T))
+#define O(T, f) printf(#T "." #f " %zu\n", offsetof(T, f))
+int main(void) {
+  P(rt_prim); O(rt_prim, p); O(rt_prim, uv); O(rt_prim, uvframe);
+  P(rt_medium); O(rt_medium, material);
+  P(rt_material); O(rt_material, param);
+  P(rt_texture); O(rt_texture, c0); O(rt_texture, params);
+  P(rt_motion); P(rt_uvframe);
+  P(rt_scene); O(rt_scene, prims); O(rt_scene, uvframes);
+  P(rt_camera_settings); O(rt_camera_settings, image_width); O(rt_camera_settings, background_c0);
+  O(rt_camera_settings, defocus_angle); O(rt_camera_settings, redirect_targets);
+  P(rt_redirect_target); P(rt_exec); P(rt_stats); O(rt_stats, samples);
+  return 0;
+}
+"""
+
+
+def test_record_layouts_match_header():
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "layout.c")
+        exe = os.path.join(d, "layout")
+        open(src, "w").write(C_LAYOUT)
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", exe, src], check=True)
+        out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout
+    c = dict(line.rsplit(" ", 1) for line in out.strip().splitlines())
+    c = {k: int(v) for k, v in c.items()}
+    assert c["rt_prim"] == S.PRIM_DTYPE.itemsize
+    assert c["rt_prim.p"] == S.PRIM_DTYPE.fields["p"][1] and c["rt_prim.uv"] == S.PRIM_DTYPE.fields["uv"][1]
+    assert c["rt_prim.uvframe"] == S.PRIM_DTYPE.fields["uvframe"][1]
+    assert c["rt_medium"] == S.MEDIUM_DTYPE.itemsize and c["rt_medium.material"] == S.MEDIUM_DTYPE.fields["material"][1]
+    assert c["rt_material"] == S.MATERIAL_DTYPE.itemsize and c["rt_material.param"] == S.MATERIAL_DTYPE.fields["param"][1]
+    assert c["rt_texture"] == S.TEXTURE_DTYPE.itemsize and c["rt_texture.c0"] == S.TEXTURE_DTYPE.fields["c0"][1]
+    assert c["rt_texture.params"] == S.TEXTURE_DTYPE.fields["params"][1]
+    assert c["rt_motion"] == S.MOTION_DTYPE.itemsize and c["rt_uvframe"] == S.UVFRAME_DTYPE.itemsize
+    assert c["rt_scene"] == ctypes.sizeof(_lib.RtScene)
+    assert c["rt_scene.uvframes"] == _lib.RtScene.uvframes.offset
+    assert c["rt_camera_settings"] == ctypes.sizeof(_lib.RtCameraSettings)
+    for f in ("image_width", "background_c0", "defocus_angle", "redirect_targets"):
+        assert c[f"rt_camera_settings.{f}"] == getattr(_lib.RtCameraSettings, f).offset, f
+    assert c["rt_redirect_target"] == ctypes.sizeof(_lib.RtRedirectTarget)
+    assert c["rt_exec"] == ctypes.sizeof(_lib.RtExec)
+    assert c["rt_stats"] == ctypes.sizeof(_lib.RtStats) and c["rt_stats.samples"] == _lib.RtStats.samples.offset
+
+
+def test_render_fails_loudly_without_a_device():
+    """No CPU fallback: on a machine without a GPU the product path raises."""
+    import torch
+    if torch.cuda.is_available():
+        return
+    import pytest
+    import raytrace_amd as R
+    from raytrace_amd import scenes
+    with pytest.raises(R.RtDeviceError):
+        R.raytrace(*scenes.cornell_box(spp=1, width=4))
+    with pytest.raises(R.RtDeviceError):
+        R.DeviceScene(scenes.cornell_box()[1])
+
+
+def test_scene_validation_errors_before_device():
+    """rt_render validates the camera before touching the device (RT_E_INVALID / UNSUPPORTED)."""
+    import pytest
+    import raytrace_amd as R
+    from raytrace_amd import scenes
+    cs, world, seed = scenes.cornell_box(spp=1, width=4)
+    with pytest.raises(R.RtInvalid):
+        R.raytrace(cs.replace(cs_samplesPerPixel=0), world, seed)
+    with pytest.raises(R.RtInvalid):
+        R.raytrace(cs.replace(cs_aspectRatio=0.0), world, seed)
+    with pytest.raises(R.RtUnsupported):
+        R.raytrace(cs.replace(cs_redirectTargets=[(0.01, (0, 0, 0), (1, 0, 0), (0, 1, 0))] * 9), world, seed)
