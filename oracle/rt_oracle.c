@@ -616,15 +616,16 @@ static v3 pixel_color(const scene_t* s, int i, int j, rng_t* r, double* cnt) {
       x = hs_random(r);
       y = hs_random(r);
     } else {
+      /* device stream: event 0 = (jitter x, jitter y, time, disk radius), event 1 = (disk angle) */
       uint32_t w0[4], w1[4];
       philox_event(r, 0, EV_CAMERA0, w0);
       philox_event(r, 0, EV_CAMERA1, w1);
-      time = u01(w0[0]);
-      double rad = sqrt(u01(w0[1])), th = 2 * PI_HS * u01(w0[2]);
+      x = u01(w0[0]);
+      y = u01(w0[1]);
+      time = u01(w0[2]);
+      double rad = sqrt(u01(w0[3])), th = 2 * PI_HS * u01(w1[0]);
       dx = rad * cos(th);
       dy = rad * sin(th);
-      x = u01(w0[3]);
-      y = u01(w1[0]);
     }
     v3 origin = add(add(s->center, smul(dx, s->disk_u)), smul(dy, s->disk_v));
     v3 target = add(add(s->top_left, smul((double)i + x, s->pixel_u)), smul((double)j + y, s->pixel_v));

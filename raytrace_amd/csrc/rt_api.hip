@@ -58,6 +58,8 @@ struct rt_device_scene {
   int n_media = 0;
   DevMedium media[RT_MAX_MEDIA];
   int n_nodes = 0, n_prims = 0, max_depth = 0;
+  int stack_depth = 1;       // LDS stack entries per lane
+  int resident_blocks = 0;   // render-kernel workgroups resident on the device at that stack depth
   double upload_ms = 0;
 };
 
@@ -129,6 +131,12 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
   s->n_nodes = H.n_nodes;
   s->n_prims = H.n_prims;
   s->max_depth = H.max_depth;
+  s->stack_depth = H.max_depth > 1 ? H.max_depth : 1;
+  s->resident_blocks = rt_render_resident_blocks(device, s->stack_depth);
+  if (s->resident_blocks <= 0) {
+    rt_scene_destroy(s);
+    return fail(RT_E_HIP, "occupancy query failed");
+  }
   s->upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = s;
   return RT_OK;
@@ -139,7 +147,7 @@ int rt_scene_stats(const rt_device_scene* s, rt_stats* st) {
   std::memset(st, 0, sizeof *st);
   st->upload_ms = s->upload_ms;
   st->bvh_nodes = s->n_nodes;
-  st->max_stack = s->max_depth;
+  st->max_stack = s->stack_depth;
   return RT_OK;
 }
 
@@ -164,10 +172,26 @@ int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint
   P.surface_root = s->surface_root;
   P.n_media = s->n_media;
   for (int k = 0; k < s->n_media; ++k) P.media[k] = s->media[k];
+  P.stack_depth = s->stack_depth;
+  rt_host_plan_work(P, (long long)s->resident_blocks * RT_BLOCK);
   HIP_TRY(hipSetDevice(s->device));
-  if (rt_launch_render(P, hip_stream))
-    return fail(RT_E_HIP, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
-  return RT_OK;
+  // stream-ordered workspace: fixed-point sums, NaN flags, queue counter (graph-capturable)
+  const size_t tile_pixels = (size_t)P.tile_rows * P.cam.width;
+  const size_t off_flag = tile_pixels * 3 * sizeof(long long);
+  const size_t off_ctr = off_flag + ((tile_pixels * sizeof(unsigned) + 255) & ~(size_t)255);
+  const size_t bytes = off_ctr + 256;
+  hipStream_t st = (hipStream_t)hip_stream;
+  char* ws = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&ws, bytes, st));
+  HIP_TRY(hipMemsetAsync(ws, 0, bytes, st));
+  P.accum = (unsigned long long*)ws;
+  P.nanflag = (unsigned int*)(ws + off_flag);
+  P.counter = (int*)(ws + off_ctr);
+  rc = RT_OK;
+  if (rt_launch_render(P, s->resident_blocks, hip_stream) || rt_launch_resolve(P, hip_stream))
+    rc = fail(RT_E_HIP, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+  HIP_TRY(hipFreeAsync(ws, st));
+  return rc;
 }
 
 int rt_render(const rt_camera_settings* cs, const rt_scene* scene, uint64_t seed, const rt_exec* ex, float* out_rgb,

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/rt.h"
@@ -317,4 +318,32 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
   P.row_block = ex->row_block;
   P.tile_rows = rows;
   return RT_OK;
+}
+
+void rt_host_plan_work(KernelParams& P, long long resident_lanes) {
+  // Items = (tile pixel, chunk of consecutive samples).  Enough items that every resident lane
+  // claims ~8 of them (the queue tail is then ~1/8 of a lane's work), but chunks of at least 4
+  // samples so the per-item refill stays cheap.  The image does not depend on this choice
+  // (fixed-point accumulation), only the schedule does.
+  const long long tile_pixels = (long long)P.tile_rows * P.cam.width;
+  const int spp = P.cam.spp;
+  long long k = tile_pixels > 0 ? (8 * resident_lanes + tile_pixels - 1) / tile_pixels : 1;
+  if (k < 1) k = 1;
+  if (k > spp) k = spp;
+  int chunk = (int)((spp + k - 1) / k);
+  const int min_chunk = spp < 4 ? spp : 4;
+  if (chunk < min_chunk) chunk = min_chunk;
+  if (const char* env = std::getenv("RT_AMD_CHUNK")) {  // tuning knob for experiments
+    int c = std::atoi(env);
+    if (c > 0) chunk = c;
+  }
+  const int n_chunks = (spp + chunk - 1) / chunk;
+  long long items = (long long)n_chunks * tile_pixels;
+  if (items > 0x7fffff00LL) {  // keep item ids in int: grow the chunk
+    chunk = (int)((long long)spp * tile_pixels / 0x7fffff00LL) + 1;
+    items = (long long)((spp + chunk - 1) / chunk) * tile_pixels;
+  }
+  P.chunk = chunk;
+  P.n_chunks = (spp + chunk - 1) / chunk;
+  P.n_items = (int)items;
 }

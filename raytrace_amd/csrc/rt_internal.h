@@ -88,6 +88,14 @@ struct KernelParams {
   const float* uvframes;   // 12 floats per frame: rows of R (xyz, -)
   float* out;
   int* status;             // device word: nonzero on stack overflow
+  // persistent-lane work queue (rt_trace.h lane_loop): items = n_chunks x tile pixels
+  unsigned long long* accum;  // 3 x int64 fixed-point (2^-32) radiance sums per tile pixel
+  unsigned int* nanflag;      // per tile pixel: a sample produced a non-finite radiance
+  int* counter;               // next unclaimed item
+  int chunk;                  // samples per item
+  int n_chunks;
+  int n_items;
+  int stack_depth;            // LDS stack entries per lane (>= the scene's BVH depth)
   int surface_root;
   int n_media;
   int n_targets;
@@ -98,6 +106,8 @@ struct KernelParams {
   uint32_t key0, key1;
   int n_shards, shard, row_block, tile_rows;
 };
+
+#define RT_FIX_SCALE 4294967296.0  // 2^32: per-sample radiance is accumulated as int64 * 2^-32
 
 // Host-side scene image, ready for upload (rt_build.cpp).
 struct HostScene {
@@ -124,5 +134,11 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
                         std::string& err);
 
 // rt_kernel.hip (device launchers)
-int rt_launch_render(const KernelParams& p, void* stream);
+// resident workgroups of the render kernel for a given LDS stack depth (occupancy query)
+int rt_render_resident_blocks(int device, int stack_depth);
+int rt_launch_render(const KernelParams& p, int grid_blocks, void* stream);
+// accum / nanflag -> out (mean over spp, NaN where flagged)
+int rt_launch_resolve(const KernelParams& p, void* stream);
+// work decomposition (rt_build.cpp): chunk so that items >= ~8 x resident lanes
+void rt_host_plan_work(KernelParams& P, long long resident_lanes);
 int rt_launch_encode8(const float* in, uint8_t* out, int64_t n, int encoding, void* stream);

@@ -1,22 +1,67 @@
-// rt_kernel.hip — MI355X (gfx950, CDNA4) kernels: the path-tracing megakernel and the 8-bit
-// output epilogue.  The per-lane logic lives in rt_trace.h.
+// rt_kernel.hip — MI355X (gfx950, CDNA4) kernels: the persistent path-tracing megakernel, the
+// fixed-point resolve, and the 8-bit output epilogue.  The per-lane logic lives in rt_trace.h.
 //
-// Launch shape: 256-lane workgroups (4 waves), one lane per tile pixel, consecutive lanes on
-// consecutive pixels of a row (coherent primary rays, coalesced output).  Each lane keeps a
-// BVH traversal stack of RT_STACK_DEPTH entries in LDS, laid out [depth][lane] so the 64
-// lanes of a wave touch 64 consecutive dwords (conflict-free).  No MFMA: the work is branchy
-// scalar FP32, not a contraction.
+// rt_render_kernel: a grid of exactly the resident workgroups (occupancy query), 256 lanes each.
+// Lanes claim (pixel, sample-chunk) items with one wave-aggregated atomicAdd per refill
+// (ballot the lanes that need work, the lowest such lane adds popcount, the base is broadcast),
+// so consecutive lanes take consecutive pixels (coherent primary rays).  Each lane keeps its
+// BVH traversal stack in LDS, laid out [depth][lane]: the 64 lanes of a wave touch 64
+// consecutive dwords (conflict-free).  The stack depth is the scene's BVH depth (dynamic LDS),
+// so shallow scenes are not occupancy-limited by LDS.  Finished items add their int64
+// fixed-point sums with 64-bit atomics (commutative: bit-exact for any schedule).
+// No MFMA: the work is branchy scalar FP32, not a contraction.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "rt_trace.h"
 
+namespace {
+
+struct WaveGrab {
+  int* counter;
+  __device__ __forceinline__ int operator()(bool need) const {
+    const unsigned long long m = __ballot(need);
+    if (m == 0ull) return 0;
+    const int lane = (int)__lane_id();
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(counter, (int)__popcll(m));
+    base = __shfl(base, leader);
+    return base + (int)__popcll(m & ((1ull << lane) - 1ull));
+  }
+};
+
+struct AtomicCommit {
+  unsigned long long* accum;
+  unsigned int* nanflag;
+  __device__ __forceinline__ void operator()(int tp, long long sx, long long sy, long long sz, bool bad) const {
+    unsigned long long* a = accum + 3 * (size_t)tp;
+    if (sx) atomicAdd(a, (unsigned long long)sx);
+    if (sy) atomicAdd(a + 1, (unsigned long long)sy);
+    if (sz) atomicAdd(a + 2, (unsigned long long)sz);
+    if (bad) atomicOr(nanflag + tp, 1u);
+  }
+};
+
+}  // namespace
+
 __global__ __launch_bounds__(RT_BLOCK) void rt_render_kernel(KernelParams P) {
-  __shared__ int stack_mem[RT_STACK_DEPTH * RT_BLOCK];
-  const int tile_pixel = blockIdx.x * RT_BLOCK + threadIdx.x;
-  if (tile_pixel >= P.tile_rows * P.cam.width) return;
-  int overflow = rtk::render_pixel(P, tile_pixel, stack_mem + threadIdx.x, RT_BLOCK);
+  extern __shared__ int stack_mem[];
+  WaveGrab grab{P.counter};
+  AtomicCommit commit{P.accum, P.nanflag};
+  int overflow = rtk::lane_loop(P, grab, commit, stack_mem + threadIdx.x, RT_BLOCK);
   if (overflow) atomicOr(P.status, 1);
+}
+
+// mean over spp (Ray.hs:232) from the fixed-point sums; NaN where a sample was non-finite
+__global__ __launch_bounds__(256) void rt_resolve_kernel(const long long* __restrict__ accum,
+                                                         const unsigned int* __restrict__ nanflag,
+                                                         float* __restrict__ out, int n_pixels, double scale) {
+  int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n_pixels) return;
+  const bool bad = nanflag[i] != 0u;
+  for (int c = 0; c < 3; ++c)
+    out[3 * (size_t)i + c] = bad ? __builtin_nanf("") : (float)((double)accum[3 * (size_t)i + c] * scale);
 }
 
 // Output epilogue of writeImage / writeImageSqrt (Ray.hs:248-260): 8-bit codes
@@ -57,11 +102,30 @@ __global__ __launch_bounds__(256) void rt_encode8_kernel(const float* __restrict
   }
 }
 
-int rt_launch_render(const KernelParams& p, void* stream) {
+int rt_render_resident_blocks(int device, int stack_depth) {
+  int per_cu = 0, cus = 0;
+  size_t lds = (size_t)stack_depth * RT_BLOCK * sizeof(int);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel, RT_BLOCK, lds) != hipSuccess) return -1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return -1;
+  if (per_cu < 1) per_cu = 1;
+  return per_cu * cus;
+}
+
+int rt_launch_render(const KernelParams& p, int grid_blocks, void* stream) {
+  if (p.n_items <= 0 || grid_blocks <= 0) return 0;
+  long long need = ((long long)p.n_items + RT_BLOCK - 1) / RT_BLOCK;
+  int grid = need < grid_blocks ? (int)need : grid_blocks;
+  size_t lds = (size_t)p.stack_depth * RT_BLOCK * sizeof(int);
+  hipLaunchKernelGGL(rt_render_kernel, dim3(grid), dim3(RT_BLOCK), lds, (hipStream_t)stream, p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int rt_launch_resolve(const KernelParams& p, void* stream) {
   int n = p.tile_rows * p.cam.width;
   if (n <= 0) return 0;
-  dim3 grid((n + RT_BLOCK - 1) / RT_BLOCK);
-  hipLaunchKernelGGL(rt_render_kernel, grid, dim3(RT_BLOCK), 0, (hipStream_t)stream, p);
+  double scale = 1.0 / (RT_FIX_SCALE * (double)p.cam.spp);
+  hipLaunchKernelGGL(rt_resolve_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     (const long long*)p.accum, p.nanflag, p.out, n, scale);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -1,8 +1,10 @@
 // rt_trace.h — the per-lane path-tracing logic of the MI355X megakernel (rt_kernel.hip).
 //
-// One lane owns one pixel and loops over its `samples_per_pixel` paths with path
-// regeneration: a lane whose path terminates immediately starts its next sample, so a
-// 64-lane wave keeps tracing until every lane has finished all its samples.  Per segment:
+// Work decomposition: the frame (this shard's rows) x spp is cut into ITEMS = (tile pixel,
+// chunk of consecutive samples).  Lanes are persistent: a lane whose item is exhausted claims
+// the next item from a global counter (one wave-aggregated atomic per refill), so every lane
+// stays busy until the queue drains and the tail is one chunk long.  Inside an item a lane
+// regenerates paths: when a path terminates the next sample starts at once.  Per segment:
 //   1. closest hit: the surface BVH (stack in LDS, near child first, reference depth-first
 //      tie-break) and, for every constantMedium, its boundary BVH (Geometry.hs:298-330);
 //   2. the material of the hit: a `switch` over the ten reference materials
@@ -10,7 +12,9 @@
 //   3. HemisphereF / SphereF: direction from the redirect mixture, weight pdf1 / pdf
 //      (Ray.hs:187-224).
 // rayColor's recursion (Ray.hs:174-224) is carried as throughput T and radiance L
-// (L = e0 + a0 (e1 + a1 (...)) = sum_k T_k e_k).
+// (L = e0 + a0 (e1 + a1 (...)) = sum_k T_k e_k).  Each sample's L is added to the pixel's sum
+// in 64-bit fixed point (2^-32): integer addition commutes, so the mean (Ray.hs:232) is bit-for-
+// bit independent of chunking, scheduling and the multi-GPU row partition.
 //
 // FP32 arithmetic; Philox4x32-10 keyed by the seed with counter (pixel, sample, segment,
 // event) and 24-bit uniforms; direct samplers in place of the reference's rejection loops
@@ -36,12 +40,16 @@ inline int f2i(float f) {
   std::memcpy(&i, &f, 4);
   return i;
 }
+// traversal counters of the host build (nodes visited, primitives tested, segments)
+extern thread_local long long counters[4];
 }  // namespace rt_emu
 #define RT_UMULHI(a, b) rt_emu::umulhi(a, b)
 #define RT_F2I(f) rt_emu::f2i(f)
 #define RT_SINCOS(x, s, c) (*(s) = sinf(x), *(c) = cosf(x))
 #define RT_LOG(x) logf(x)
 #define RT_RSQRT(x) (1.0f / sqrtf(x))
+#define RT_RCP(x) (1.0f / (x))
+#define RT_COUNT(i) (++rt_emu::counters[i])
 #else
 #define RT_FN __device__ __forceinline__
 #define RT_UMULHI(a, b) __umulhi(a, b)
@@ -49,6 +57,8 @@ inline int f2i(float f) {
 #define RT_SINCOS(x, s, c) __sincosf(x, s, c)
 #define RT_LOG(x) __logf(x)
 #define RT_RSQRT(x) __frsqrt_rn(x)
+#define RT_RCP(x) __builtin_amdgcn_rcpf(x)
+#define RT_COUNT(i) ((void)0)
 #endif
 
 namespace rtk {
@@ -62,9 +72,6 @@ struct alignas(16) v4 {
 };
 struct alignas(16) i4 {
   int x, y, z, w;
-};
-struct alignas(8) v2 {
-  float x, y;
 };
 struct f3 {
   float x, y, z;
@@ -130,6 +137,8 @@ RT_FN f3 motion_shift(const KernelParams& P, int m, float time) {
   return (1.0f - time) * v0 + time * v1;
 }
 
+RT_FN float safe_rcp(float d) { return RT_RCP(fabsf(d) > 1e-20f ? d : copysignf(1e-20f, d)); }
+
 // Closest hit within (tmin, tbest) over one BVH; ties go to the smaller depth-first `order`
 // (the reference's group / bvhNode tie-break).  stack[k * stride] is this lane's stack.
 RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmin, float& tbest, int& best,
@@ -139,6 +148,7 @@ RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmi
   int node = root;
   for (;;) {
     if (node >= 0) {
+      RT_COUNT(0);
       const float* nd = P.nodes + 16 * (size_t)node;
       v4 n0 = ld4(nd), n1 = ld4(nd + 4), n2 = ld4(nd + 8);
       i4 n3 = *reinterpret_cast<const i4*>(nd + 12);
@@ -159,7 +169,7 @@ RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmi
           nearc = n3.y;
           farc = n3.x;
         }
-        if (sp < RT_STACK_DEPTH) {
+        if (sp < P.stack_depth) {
           stack[sp * stride] = farc;
           ++sp;
         } else {
@@ -180,6 +190,7 @@ RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmi
       int enc = ~node;
       int first = enc >> 4, count = (enc & 15) + 1;
       for (int k = 0; k < count; ++k) {
+        RT_COUNT(1);
         int pi = first + k;
         const float* pr = P.prims + 16 * (size_t)pi;
         v4 a = ld4(pr), b = ld4(pr + 4);
@@ -211,7 +222,7 @@ RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmi
           float denom = dot(n, R.d);
           if (!(fabsf(denom) > 1e-8f)) continue;
           f3 qo = xyz(b) - o;
-          t = dot(n, qo) / denom;
+          t = dot(n, qo) * RT_RCP(denom);
           if (!(t > tmin && t <= tbest && t < kInf)) continue;
           v4 c = ld4(pr + 8), e = ld4(pr + 12);
           f3 prel = t * R.d - qo;
@@ -267,7 +278,7 @@ RT_FN HitInfo surface_info(const KernelParams& P, int pi, const RayCtx& R, float
   if ((kf & RT_KIND_MASK) == 0) {
     f3 c = xyz(a);
     if (kf & RT_FLAG_MOTION) c = c + motion_shift(P, RT_F2I(pr[15]), R.time);
-    f3 outward = (1.0f / b.x) * (h.p - c);
+    f3 outward = RT_RCP(b.x) * (h.p - c);
     h.front = dot(R.d, outward) <= 0.0f;
     h.n = h.front ? outward : -outward;
     int uvf = RT_F2I(b.z);
@@ -311,50 +322,74 @@ RT_FN bool target_hit(const DevTarget& T, f3 o, f3 d, float& t) {
   float denom = dot(n, d);
   if (!(fabsf(denom) > 1e-8f)) return false;
   f3 qo = ld3(T.q) - o;
-  t = dot(n, qo) / denom;
+  t = dot(n, qo) * RT_RCP(denom);
   if (!(t > 0.0f)) return false;
   f3 prel = t * d - qo;
   float a = dot(prel, ld3(T.wa)), b = dot(prel, ld3(T.wb));
   return a >= 0.0f && a <= 1.0f && b >= 0.0f && b <= 1.0f;
 }
 
-// All samples of one tile pixel; writes the mean colour.  Returns the stack-overflow flag.
-RT_FN int render_pixel(const KernelParams& P, int tile_pixel, int* stack, int stride) {
-  int overflow = 0;
-  const int W = P.cam.width;
-  const int tr = tile_pixel / W, px = tile_pixel - tr * W;
-  const int gy = ((tr / P.row_block) * P.n_shards + P.shard) * P.row_block + (tr % P.row_block);
-  float* out = P.out + 3 * (size_t)tile_pixel;
-  if (gy >= P.cam.height) {  // padding row of the shard
-    out[0] = 0.0f;
-    out[1] = 0.0f;
-    out[2] = 0.0f;
+// per-sample radiance -> 64-bit fixed point (2^-32); non-finite values set the pixel's flag
+RT_FN long long to_fixed(float x, bool& bad) {
+  if (!(fabsf(x) < 1.0e9f)) {
+    bad = true;
     return 0;
   }
-  const uint32_t pix = (uint32_t)(gy * W + px);
-  const int spp = P.cam.spp, max_depth = P.cam.max_depth;
-  const f3 center = ld3(P.cam.center), top_left = ld3(P.cam.top_left), pu = ld3(P.cam.pixel_u),
-           pv = ld3(P.cam.pixel_v), du = ld3(P.cam.disk_u), dv = ld3(P.cam.disk_v);
+  return (long long)((double)x * RT_FIX_SCALE);
+}
 
-  f3 acc = mk3(0.f, 0.f, 0.f);
-  f3 L = acc, T = mk3(1.f, 1.f, 1.f);
+// The persistent lane loop.  `grab(need)` is wave-collective: it returns a fresh item for
+// lanes with need == true.  `commit(tile_pixel, sx, sy, sz, bad)` adds a finished item's sums.
+template <class Grab, class Commit>
+RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, int* stack, int stride) {
+  int overflow = 0;
+  const int W = P.cam.width, tile_pixels = P.tile_rows * W;
+  const int spp = P.cam.spp, max_depth = P.cam.max_depth;
+  int item = -1, tp = 0, sample = 0, s_end = 0, seg = 0;
+  int px = 0, gy = 0;
+  uint32_t pix = 0;
+  long long sx = 0, sy = 0, sz = 0;
+  bool bad = false;
+  bool alive = false;
+  f3 L = mk3(0.f, 0.f, 0.f), T = mk3(1.f, 1.f, 1.f);
   RayCtx R;
-  R.o = R.d = R.idir = R.oidir = acc;
+  R.o = R.d = R.idir = R.oidir = L;
   R.time = 0.0f;
   R.self_gid = -1;
-  int sample = 0, seg = 0;
-  bool alive = false;
   for (;;) {
+    const bool need = !alive && sample >= s_end;
+    if (need && item >= 0) commit(tp, sx, sy, sz, bad);
+    const int got = grab(need);
+    if (need) {
+      item = got;
+      if (item >= P.n_items) break;
+      const int k = item / tile_pixels;
+      tp = item - k * tile_pixels;
+      const int tr = tp / W;
+      px = tp - tr * W;
+      gy = ((tr / P.row_block) * P.n_shards + P.shard) * P.row_block + (tr % P.row_block);
+      pix = (uint32_t)(gy * W + px);
+      sample = k * P.chunk;
+      s_end = sample + P.chunk < spp ? sample + P.chunk : spp;
+      if (gy >= P.cam.height || max_depth <= 0) s_end = sample;  // padding row / black image
+      sx = sy = sz = 0;
+      bad = false;
+      if (sample >= s_end) continue;
+    }
     if (!alive) {
-      if (sample >= spp || max_depth <= 0) break;
-      // Ray.hs:157-172, 229: time, defocus-disk point, pixel jitter
+      // Ray.hs:157-172, 229: pixel jitter, time, defocus-disk point
       u4 w0 = philox(pix, (uint32_t)sample, 0u, RT_EV_CAMERA0, P.key0, P.key1);
-      u4 w1 = philox(pix, (uint32_t)sample, 0u, RT_EV_CAMERA1, P.key0, P.key1);
-      R.time = u01(w0.x);
-      float rad = sqrtf(u01(w0.y)), s, c;
-      RT_SINCOS(2.0f * kPi * u01(w0.z), &s, &c);
-      f3 origin = center + (rad * c) * du + (rad * s) * dv;
-      f3 target = top_left + ((float)px + u01(w0.w)) * pu + ((float)gy + u01(w1.x)) * pv;
+      R.time = u01(w0.z);
+      f3 origin = ld3(P.cam.center);
+      if (P.cam.disk_u[0] != 0.0f || P.cam.disk_u[1] != 0.0f || P.cam.disk_u[2] != 0.0f ||
+          P.cam.disk_v[0] != 0.0f || P.cam.disk_v[1] != 0.0f || P.cam.disk_v[2] != 0.0f) {
+        u4 w1 = philox(pix, (uint32_t)sample, 0u, RT_EV_CAMERA1, P.key0, P.key1);
+        float rad = sqrtf(u01(w0.w)), s, c;
+        RT_SINCOS(2.0f * kPi * u01(w1.x), &s, &c);
+        origin = origin + (rad * c) * ld3(P.cam.disk_u) + (rad * s) * ld3(P.cam.disk_v);
+      }
+      f3 target = ld3(P.cam.top_left) + ((float)px + u01(w0.x)) * ld3(P.cam.pixel_u) +
+                  ((float)gy + u01(w0.y)) * ld3(P.cam.pixel_v);
       R.o = origin;
       R.d = normalize(target - origin);
       R.self_gid = -1;
@@ -363,10 +398,9 @@ RT_FN int render_pixel(const KernelParams& P, int tile_pixel, int* stack, int st
       seg = 0;
       alive = true;
     }
+    RT_COUNT(2);
     // ---- closest hit over the surfaces and every medium (Ray.hs:178)
-    R.idir = mk3(1.0f / (fabsf(R.d.x) > 1e-20f ? R.d.x : copysignf(1e-20f, R.d.x)),
-                 1.0f / (fabsf(R.d.y) > 1e-20f ? R.d.y : copysignf(1e-20f, R.d.y)),
-                 1.0f / (fabsf(R.d.z) > 1e-20f ? R.d.z : copysignf(1e-20f, R.d.z)));
+    R.idir = mk3(safe_rcp(R.d.x), safe_rcp(R.d.y), safe_rcp(R.d.z));
     R.oidir = R.o * R.idir;
     float tbest = kInf;
     int best = -1, best_order = 0x7fffffff;
@@ -455,10 +489,10 @@ RT_FN int render_pixel(const KernelParams& P, int tile_pixel, int* stack, int st
         }
         case 6: {  // dielectric
           float ior = Mt.param;
-          float ratio = h.front ? 1.0f / ior : ior;
+          float ratio = h.front ? RT_RCP(ior) : ior;
           float cos_t = fminf(1.0f, -dot(h.n, R.d));
           float sin_t = sqrtf(fmaxf(0.0f, 1.0f - cos_t * cos_t));
-          float r0 = (1.0f - ratio) / (1.0f + ratio);
+          float r0 = (1.0f - ratio) * RT_RCP(1.0f + ratio);
           r0 = r0 * r0;
           float x1 = 1.0f - cos_t, x2 = x1 * x1;
           float reflectance = r0 + (1.0f - r0) * (x2 * x2 * x1);
@@ -501,19 +535,19 @@ RT_FN int render_pixel(const KernelParams& P, int tile_pixel, int* stack, int st
           for (int k = 0; k < P.n_targets; ++k) {
             float tt;
             if (target_hit(P.targets[k], h.p, dir, tt))
-              mix += P.targets[k].prob * (tt * tt / fabsf(dot(ld3(P.targets[k].cr), dir)));
+              mix += P.targets[k].prob * (tt * tt * RT_RCP(fabsf(dot(ld3(P.targets[k].cr), dir))));
           }
           float pdf = P.rem_prob * pdf1 + mix;
           f3 f = eval_texture(P, Mt.tex, h.u, h.v);
           if (Mt.kind == 3) {
             float mu0 = -dot(R.d, h.n), mu1 = dot(dir, h.n);
-            f = (0.25f / (mu0 + mu1)) * f;
+            f = (0.25f * RT_RCP(mu0 + mu1)) * f;
           } else if (Mt.kind == 9) {
             float g = Mt.param, mu = dot(R.d, dir);
             float base = 1.0f + g * g - 2.0f * g * mu;
-            f = ((1.0f - g * g) / (base * sqrtf(base))) * f;
+            f = ((1.0f - g * g) * RT_RCP(base * sqrtf(base))) * f;
           }
-          T = T * ((pdf1 / pdf) * f);
+          T = T * ((pdf1 * RT_RCP(pdf)) * f);
           newdir = dir;
           break;
         }
@@ -530,15 +564,13 @@ RT_FN int render_pixel(const KernelParams& P, int tile_pixel, int* stack, int st
       }
     }
     if (terminate) {
-      acc = acc + L;
+      sx += to_fixed(L.x, bad);
+      sy += to_fixed(L.y, bad);
+      sz += to_fixed(L.z, bad);
       alive = false;
       ++sample;
     }
   }
-  const float inv = 1.0f / (float)spp;
-  out[0] = acc.x * inv;
-  out[1] = acc.y * inv;
-  out[2] = acc.z * inv;
   return overflow;
 }
 

@@ -23,7 +23,7 @@ def lib():
     return _lib
 
 
-def render(settings, world, seed, n_shards=1, shard=0, row_block=4, nthreads=None):
+def render(settings, world, seed, n_shards=1, shard=0, row_block=4, nthreads=None, chunk=0, counters=False):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
     from raytrace_amd import _lib as R
@@ -38,8 +38,12 @@ def render(settings, world, seed, n_shards=1, shard=0, row_block=4, nthreads=Non
     rows = shard_rows(h, n_shards, row_block)
     out = np.zeros((rows, int(settings.cs_imageWidth), 3), np.float32)
     L = lib()
+    cnt = np.zeros(4, np.int64)
     rc = L.rt_emu_render(ctypes.byref(cs), ctypes.byref(sc), ctypes.c_uint64(_seed64(seed)), ctypes.byref(ex),
-                         out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(nthreads or min(16, os.cpu_count() or 1)))
+                         out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(nthreads or min(16, os.cpu_count() or 1)),
+                         ctypes.c_int(chunk), cnt.ctypes.data_as(ctypes.c_void_p))
     if rc != 0:
         raise RuntimeError(f"rt_emu_render failed {rc}: {L.rt_emu_last_error().decode()}")
+    if counters:
+        return out, dict(zip(["bvh_nodes", "prims_tested", "segments", "samples"], cnt.tolist()))
     return out

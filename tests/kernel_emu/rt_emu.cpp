@@ -5,6 +5,7 @@
 #include <pthread.h>
 
 #include <atomic>
+#include <cmath>
 #include <string>
 #include <vector>
 
@@ -12,24 +13,44 @@
 #include "../../raytrace_amd/csrc/rt_internal.h"
 #include "../../raytrace_amd/csrc/rt_trace.h"
 
+namespace rt_emu {
+thread_local long long counters[4];
+}
+
 namespace {
 thread_local std::string g_err;
 
-struct Job {
+struct Shared {
   const KernelParams* P;
-  int n;
   std::atomic<int> next{0};
   std::atomic<int> overflow{0};
+  std::vector<std::atomic<long long>>* accum;
+  std::vector<std::atomic<unsigned>>* flags;
+  std::atomic<long long> cnt[4];
+};
+
+struct Grab {
+  Shared* s;
+  int operator()(bool need) { return need ? s->next.fetch_add(1) : 0; }
+};
+struct Commit {
+  Shared* s;
+  void operator()(int tp, long long x, long long y, long long z, bool bad) {
+    (*s->accum)[3 * (size_t)tp] += x;
+    (*s->accum)[3 * (size_t)tp + 1] += y;
+    (*s->accum)[3 * (size_t)tp + 2] += z;
+    if (bad) (*s->flags)[tp] |= 1u;
+  }
 };
 
 void* worker(void* arg) {
-  Job* j = (Job*)arg;
-  int stack[RT_STACK_DEPTH];
-  for (;;) {
-    int k = j->next.fetch_add(1);
-    if (k >= j->n) break;
-    if (rtk::render_pixel(*j->P, k, stack, 1)) j->overflow = 1;
-  }
+  Shared* s = (Shared*)arg;
+  std::vector<int> stack(s->P->stack_depth);
+  for (auto& c : rt_emu::counters) c = 0;
+  Grab g{s};
+  Commit c{s};
+  if (rtk::lane_loop(*s->P, g, c, stack.data(), 1)) s->overflow = 1;
+  for (int i = 0; i < 4; ++i) s->cnt[i] += rt_emu::counters[i];
   return nullptr;
 }
 }  // namespace
@@ -37,8 +58,9 @@ void* worker(void* arg) {
 extern "C" {
 const char* rt_emu_last_error(void) { return g_err.c_str(); }
 
+// counters (optional, 4 values): BVH nodes visited, primitives tested, segments, samples
 int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t seed, const rt_exec* ex, float* out,
-                  int nthreads) {
+                  int nthreads, int chunk, long long* counters) {
   HostScene H;
   int rc = rt_host_build_scene(sc, H, g_err);
   if (rc) return rc;
@@ -57,16 +79,38 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
   P.surface_root = H.surface_root;
   P.n_media = H.n_media;
   for (int k = 0; k < H.n_media; ++k) P.media[k] = H.media[k];
-  Job j;
-  j.P = &P;
-  j.n = P.tile_rows * P.cam.width;
+  P.stack_depth = H.max_depth > 1 ? H.max_depth : 1;
+  rt_host_plan_work(P, 4096);
+  if (chunk > 0) {
+    P.chunk = chunk;
+    P.n_chunks = (P.cam.spp + chunk - 1) / chunk;
+    P.n_items = P.n_chunks * P.tile_rows * P.cam.width;
+  }
+  const size_t tile_pixels = (size_t)P.tile_rows * P.cam.width;
+  std::vector<std::atomic<long long>> accum(tile_pixels * 3);
+  std::vector<std::atomic<unsigned>> flags(tile_pixels);
+  for (auto& a : accum) a = 0;
+  for (auto& f : flags) f = 0;
+  Shared s;
+  s.P = &P;
+  s.accum = &accum;
+  s.flags = &flags;
+  for (auto& c : s.cnt) c = 0;
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 64) nthreads = 64;
   pthread_t th[64];
-  for (int t = 1; t < nthreads; ++t) pthread_create(&th[t], nullptr, worker, &j);
-  worker(&j);
+  for (int t = 1; t < nthreads; ++t) pthread_create(&th[t], nullptr, worker, &s);
+  worker(&s);
   for (int t = 1; t < nthreads; ++t) pthread_join(th[t], nullptr);
-  if (j.overflow) {
+  const double scale = 1.0 / (RT_FIX_SCALE * (double)P.cam.spp);
+  for (size_t i = 0; i < tile_pixels; ++i)
+    for (int c = 0; c < 3; ++c)
+      out[3 * i + c] = flags[i] ? NAN : (float)((double)accum[3 * i + c].load() * scale);
+  if (counters) {
+    for (int i = 0; i < 3; ++i) counters[i] = s.cnt[i];
+    counters[3] = (long long)tile_pixels * P.cam.spp;
+  }
+  if (s.overflow) {
     g_err = "BVH traversal stack overflow";
     return RT_E_STACK;
   }
