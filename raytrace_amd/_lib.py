@@ -10,7 +10,7 @@ import numpy as np
 from .errors import RtDeviceError, RtError, RtInvalid, RtUnsupported
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "librt_amd.so")
+LIB_PATH = os.environ.get("RT_AMD_LIB") or os.path.join(HERE, "_lib", "librt_amd.so")  # env: experiment builds
 
 RT_OK, RT_E_GENERIC, RT_E_INVALID, RT_E_UNSUPPORTED, RT_E_HIP, RT_E_STACK = 0, -1, -2, -3, -4, -5
 

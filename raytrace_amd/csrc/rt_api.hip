@@ -5,6 +5,7 @@
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -59,6 +60,7 @@ struct rt_device_scene {
   DevMedium media[RT_MAX_MEDIA];
   int n_nodes = 0, n_prims = 0, max_depth = 0;
   int stack_depth = 1;       // LDS stack entries per lane
+  bool flat = false;         // all sets are flat leaves: the LDS-resident variant
   int resident_blocks = 0;   // render-kernel workgroups resident on the device at that stack depth
   double upload_ms = 0;
 };
@@ -132,7 +134,8 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
   s->n_prims = H.n_prims;
   s->max_depth = H.max_depth;
   s->stack_depth = H.max_depth > 1 ? H.max_depth : 1;
-  s->resident_blocks = rt_render_resident_blocks(device, s->stack_depth);
+  s->flat = H.flat && std::getenv("RT_AMD_NO_FLAT") == nullptr;
+  s->resident_blocks = rt_render_resident_blocks(device, s->stack_depth, s->flat, H.n_prims);
   if (s->resident_blocks <= 0) {
     rt_scene_destroy(s);
     return fail(RT_E_HIP, "occupancy query failed");
@@ -173,6 +176,7 @@ int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint
   P.n_media = s->n_media;
   for (int k = 0; k < s->n_media; ++k) P.media[k] = s->media[k];
   P.stack_depth = s->stack_depth;
+  P.n_prims = s->n_prims;
   rt_host_plan_work(P, (long long)s->resident_blocks * RT_BLOCK);
   HIP_TRY(hipSetDevice(s->device));
   // stream-ordered workspace: fixed-point sums, NaN flags, queue counter (graph-capturable)
@@ -188,7 +192,7 @@ int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint
   P.nanflag = (unsigned int*)(ws + off_flag);
   P.counter = (int*)(ws + off_ctr);
   rc = RT_OK;
-  if (rt_launch_render(P, s->resident_blocks, hip_stream) || rt_launch_resolve(P, hip_stream))
+  if (rt_launch_render(P, s->resident_blocks, s->flat, hip_stream) || rt_launch_resolve(P, hip_stream))
     rc = fail(RT_E_HIP, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
   HIP_TRY(hipFreeAsync(ws, st));
   return rc;

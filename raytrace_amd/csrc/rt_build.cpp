@@ -240,6 +240,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   }
   S.n_nodes = (int)(S.nodes.size() / 16);
   S.n_prims = n;
+  S.flat = S.n_nodes == 0 && n <= RT_LDS_PRIMS_MAX;
   return RT_OK;
 }
 
@@ -321,18 +322,15 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
 }
 
 void rt_host_plan_work(KernelParams& P, long long resident_lanes) {
-  // Items = (tile pixel, chunk of consecutive samples).  Enough items that every resident lane
-  // claims ~8 of them (the queue tail is then ~1/8 of a lane's work), but chunks of at least 4
-  // samples so the per-item refill stays cheap.  The image does not depend on this choice
-  // (fixed-point accumulation), only the schedule does.
+  // Items = (tile pixel, chunk of consecutive samples), claimed in pixel order.  Small chunks
+  // keep the 64 lanes of a wave on neighbouring pixels (coherent rays) and make the queue tail
+  // short; below ~2 samples the per-item commit (3 atomics) dominates.  Measured on MI355X,
+  // Cornell 600x600x200 (tools/sweep_chunk.sh): 1 -> 14.3 ms, 2 -> 8.70, 4 -> 8.79, 8 -> 8.97,
+  // 34 -> 10.3, 200 -> 16.5.  The image does not depend on this choice (fixed-point sums).
+  (void)resident_lanes;
   const long long tile_pixels = (long long)P.tile_rows * P.cam.width;
   const int spp = P.cam.spp;
-  long long k = tile_pixels > 0 ? (8 * resident_lanes + tile_pixels - 1) / tile_pixels : 1;
-  if (k < 1) k = 1;
-  if (k > spp) k = spp;
-  int chunk = (int)((spp + k - 1) / k);
-  const int min_chunk = spp < 4 ? spp : 4;
-  if (chunk < min_chunk) chunk = min_chunk;
+  int chunk = spp < 4 ? spp : 4;
   if (const char* env = std::getenv("RT_AMD_CHUNK")) {  // tuning knob for experiments
     int c = std::atoi(env);
     if (c > 0) chunk = c;

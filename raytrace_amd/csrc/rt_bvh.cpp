@@ -56,7 +56,7 @@ struct Builder {
     tmp.emplace_back();
     tmp[id].box = bounds(b, e);
     int n = e - b;
-    if (n <= 2) {
+    if (n <= 2 || (depth == 0 && n <= RT_FLAT_MAX)) {  // tiny sets: one flat, coherent leaf
       tmp[id].first = b;
       tmp[id].count = n;
       return id;
@@ -182,8 +182,8 @@ void rt_build_bvh(std::vector<BuildPrim> prims, int node_base, int prim_base, Bv
   auto enc = [&](int id) -> int {
     const Node& nd = B.tmp[id];
     if (nd.left >= 0) return dev_index[id];
-    // leaf: ~(first * 16 + count - 1); counts above 16 cannot occur (leaves hold <= RT_LEAF_MAX)
-    return ~((prim_base + nd.first) * 16 + (nd.count - 1));
+    // leaf: ~(first << RT_LEAF_SHIFT | count - 1); leaves hold <= RT_FLAT_MAX primitives
+    return ~(((prim_base + nd.first) << RT_LEAF_SHIFT) | (nd.count - 1));
   };
   out.n_nodes = (int)internal.size();
   out.nodes.assign((size_t)out.n_nodes * 16, 0.0f);

@@ -8,7 +8,7 @@
 //               [1] = (R.lo.x, R.hi.x, R.lo.y, R.hi.y)
 //               [2] = (L.lo.z, L.hi.z, R.lo.z, R.hi.z)
 //               [3] = (left child, right child, -, -) as int bits; child >= 0 is a node,
-//                     child < 0 is a leaf ~(first * 16 + count - 1)
+//                     child < 0 is a leaf ~(first * 64 + count - 1)
 //   prims   : 4 x float4 per primitive (reordered into BVH leaf order, set after set)
 //               plane : [0] = (n.xyz, kindflags) [1] = (q.xyz, gid) [2] = (wa.xyz, order)
 //                       [3] = (wb.xyz, motion)   with a = (p-q).wa, b = (p-q).wb (Geometry.hs:130-131)
@@ -27,6 +27,9 @@
 #define RT_MAX_MEDIA 8
 #define RT_MAX_TARGETS 8
 #define RT_LEAF_MAX 8
+#define RT_LEAF_SHIFT 6       // leaf encoding ~(first << 6 | count - 1), count <= 64
+#define RT_FLAT_MAX 32        // a set of at most this many leaves is one flat leaf (no traversal)
+#define RT_LDS_PRIMS_MAX 256  // flat scenes whose leaves fit (16 KB) are staged in LDS
 #define RT_EMPTY_ROOT ((int)0x80000000)
 
 #define RT_KIND_MASK 3
@@ -96,6 +99,7 @@ struct KernelParams {
   int n_chunks;
   int n_items;
   int stack_depth;            // LDS stack entries per lane (>= the scene's BVH depth)
+  int n_prims;                // all leaves (every set), staged in LDS by the flat kernel
   int surface_root;
   int n_media;
   int n_targets;
@@ -119,6 +123,7 @@ struct HostScene {
   int n_media = 0;
   DevMedium media[RT_MAX_MEDIA];
   int n_nodes = 0, n_prims = 0, max_depth = 0;
+  bool flat = false;  // every set is a single flat leaf (no BVH nodes)
 };
 
 struct rt_scene;
@@ -135,8 +140,9 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
 
 // rt_kernel.hip (device launchers)
 // resident workgroups of the render kernel for a given LDS stack depth (occupancy query)
-int rt_render_resident_blocks(int device, int stack_depth);
-int rt_launch_render(const KernelParams& p, int grid_blocks, void* stream);
+// flat: the variant for scenes whose sets are all single flat leaves (prims staged in LDS)
+int rt_render_resident_blocks(int device, int stack_depth, bool flat, int n_prims);
+int rt_launch_render(const KernelParams& p, int grid_blocks, bool flat, void* stream);
 // accum / nanflag -> out (mean over spp, NaN where flagged)
 int rt_launch_resolve(const KernelParams& p, void* stream);
 // work decomposition (rt_build.cpp): chunk so that items >= ~8 x resident lanes

@@ -17,17 +17,38 @@
 
 namespace {
 
+// Item claims.  A wave keeps a pool of consecutive item ids in SGPRs (wave-uniform state) and
+// refills it with ONE returning atomicAdd of RT_POOL ids, so the global head word sees one
+// atomic per 64 claims instead of one per refilling wave-iteration (a single word saturates at
+// ~88 returning atomics per microsecond, MI355X_MICROARCH.md "dequeue").  Lanes that need work
+// take ids in lane order; ids are never dropped (a pool is contiguous and increasing, so once a
+// lane draws an id >= n_items every later id is out of range too).
+#define RT_POOL 64
 struct WaveGrab {
   int* counter;
-  __device__ __forceinline__ int operator()(bool need) const {
+  int pool_base;
+  int pool_left;
+  __device__ __forceinline__ int operator()(bool need) {
     const unsigned long long m = __ballot(need);
     if (m == 0ull) return 0;
     const int lane = (int)__lane_id();
-    const int leader = __ffsll((unsigned long long)m) - 1;
-    int base = 0;
-    if (lane == leader) base = atomicAdd(counter, (int)__popcll(m));
-    base = __shfl(base, leader);
-    return base + (int)__popcll(m & ((1ull << lane) - 1ull));
+    const int cnt = (int)__popcll(m);
+    const int rank = (int)__popcll(m & ((1ull << lane) - 1ull));
+    int item;
+    if (pool_left >= cnt) {
+      item = pool_base + rank;
+      pool_base += cnt;
+      pool_left -= cnt;
+    } else {
+      int base = 0;
+      if (lane == __ffsll((unsigned long long)m) - 1) base = atomicAdd(counter, RT_POOL);
+      base = __builtin_amdgcn_readfirstlane(__shfl(base, __ffsll((unsigned long long)m) - 1));
+      item = rank < pool_left ? pool_base + rank : base + (rank - pool_left);
+      const int used = cnt - pool_left;
+      pool_base = base + used;
+      pool_left = RT_POOL - used;
+    }
+    return item;
   }
 };
 
@@ -45,11 +66,25 @@ struct AtomicCommit {
 
 }  // namespace
 
-__global__ __launch_bounds__(RT_BLOCK) void rt_render_kernel(KernelParams P) {
-  extern __shared__ int stack_mem[];
-  WaveGrab grab{P.counter};
+// kFlat = false: BVH scenes, dynamic LDS = the lanes' traversal stacks [depth][lane].
+// kFlat = true: every primitive set is one flat leaf; no LDS: the records are read with
+// wave-uniform addresses (scalar loads into SGPRs, scalar-cache resident).
+#ifdef RT_EXP_WAVES  // ablation: force waves per SIMD (register cap)
+#define RT_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(RT_EXP_WAVES, RT_EXP_WAVES)))
+#else
+#define RT_WAVES_ATTR
+#endif
+template <bool kFlat>
+__global__ __launch_bounds__(RT_BLOCK) RT_WAVES_ATTR void rt_render_kernel(KernelParams P) {
+  extern __shared__ int smem[];
+  WaveGrab grab{P.counter, 0, 0};
   AtomicCommit commit{P.accum, P.nanflag};
-  int overflow = rtk::lane_loop(P, grab, commit, stack_mem + threadIdx.x, RT_BLOCK);
+  int overflow;
+  if constexpr (kFlat) {
+    overflow = rtk::lane_loop<true>(P, grab, commit, nullptr, 0, P.prims);
+  } else {
+    overflow = rtk::lane_loop<false>(P, grab, commit, smem + threadIdx.x, RT_BLOCK, P.prims);
+  }
   if (overflow) atomicOr(P.status, 1);
 }
 
@@ -102,21 +137,31 @@ __global__ __launch_bounds__(256) void rt_encode8_kernel(const float* __restrict
   }
 }
 
-int rt_render_resident_blocks(int device, int stack_depth) {
+static size_t render_lds_bytes(int stack_depth, bool flat, int n_prims) {
+  (void)n_prims;
+  return flat ? 0 : (size_t)stack_depth * RT_BLOCK * sizeof(int);
+}
+
+int rt_render_resident_blocks(int device, int stack_depth, bool flat, int n_prims) {
   int per_cu = 0, cus = 0;
-  size_t lds = (size_t)stack_depth * RT_BLOCK * sizeof(int);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel, RT_BLOCK, lds) != hipSuccess) return -1;
+  size_t lds = render_lds_bytes(stack_depth, flat, n_prims);
+  hipError_t e = flat ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<true>, RT_BLOCK, lds)
+                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<false>, RT_BLOCK, lds);
+  if (e != hipSuccess) return -1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return -1;
   if (per_cu < 1) per_cu = 1;
   return per_cu * cus;
 }
 
-int rt_launch_render(const KernelParams& p, int grid_blocks, void* stream) {
+int rt_launch_render(const KernelParams& p, int grid_blocks, bool flat, void* stream) {
   if (p.n_items <= 0 || grid_blocks <= 0) return 0;
   long long need = ((long long)p.n_items + RT_BLOCK - 1) / RT_BLOCK;
   int grid = need < grid_blocks ? (int)need : grid_blocks;
-  size_t lds = (size_t)p.stack_depth * RT_BLOCK * sizeof(int);
-  hipLaunchKernelGGL(rt_render_kernel, dim3(grid), dim3(RT_BLOCK), lds, (hipStream_t)stream, p);
+  size_t lds = render_lds_bytes(p.stack_depth, flat, p.n_prims);
+  if (flat)
+    hipLaunchKernelGGL(rt_render_kernel<true>, dim3(grid), dim3(RT_BLOCK), lds, (hipStream_t)stream, p);
+  else
+    hipLaunchKernelGGL(rt_render_kernel<false>, dim3(grid), dim3(RT_BLOCK), lds, (hipStream_t)stream, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -50,6 +50,7 @@ extern thread_local long long counters[4];
 #define RT_RSQRT(x) (1.0f / sqrtf(x))
 #define RT_RCP(x) (1.0f / (x))
 #define RT_COUNT(i) (++rt_emu::counters[i])
+#define RT_CAS
 #else
 #define RT_FN __device__ __forceinline__
 #define RT_UMULHI(a, b) __umulhi(a, b)
@@ -59,6 +60,10 @@ extern thread_local long long counters[4];
 #define RT_RSQRT(x) __frsqrt_rn(x)
 #define RT_RCP(x) __builtin_amdgcn_rcpf(x)
 #define RT_COUNT(i) ((void)0)
+// Scene data is read through the constant address space: the kernel never writes it, so
+// wave-uniform reads (flat sets, kernel-argument indices) become scalar loads into SGPRs and
+// divergent reads stay vector loads.
+#define RT_CAS __attribute__((address_space(4)))
 #endif
 
 namespace rtk {
@@ -92,14 +97,25 @@ RT_FN f3 normalize(f3 v) {
 RT_FN f3 reflect(f3 n, f3 v) { return v - (2.0f * dot(n, v)) * n; }  // Core.hs:49-51
 RT_FN f3 xyz(v4 v) { return f3{v.x, v.y, v.z}; }
 RT_FN v4 ld4(const float* p) { return *reinterpret_cast<const v4*>(p); }
+typedef const RT_CAS float* cfp;  // pointer to read-only scene data
+RT_FN cfp cf(const float* p) { return (cfp)p; }
+RT_FN f3 ldc3(cfp p) { return f3{p[0], p[1], p[2]}; }
+RT_FN v4 ldc4(cfp p) {
+  const RT_CAS v4* q = (const RT_CAS v4*)p;
+  return v4{q->x, q->y, q->z, q->w};
+}
+RT_FN int ldci(const int* p, int i) { return ((const RT_CAS int*)p)[i]; }
 
 // ------------------------------------------------------------------ Philox4x32-10
 struct u4 {
   uint32_t x, y, z, w;
 };
 RT_FN u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#ifndef RT_PHILOX_ROUNDS
+#define RT_PHILOX_ROUNDS 10
+#endif
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < RT_PHILOX_ROUNDS; ++r) {
     if (r) {
       k0 += 0x9E3779B9u;
       k1 += 0xBB67AE85u;
@@ -122,7 +138,12 @@ RT_FN f3 unit_vector(uint32_t a, uint32_t b) {
   float z = 1.0f - 2.0f * u01(a);
   float r = sqrtf(fmaxf(0.0f, 1.0f - z * z));
   float s, c;
+#ifdef RT_EXP_NO_SINCOS  // ablation: wrong directions, measures the cost of sincos
+  c = 1.0f - 2.0f * u01(b);
+  s = sqrtf(fmaxf(0.0f, 1.0f - c * c));
+#else
   RT_SINCOS(2.0f * kPi * u01(b), &s, &c);
+#endif
   return mk3(r * c, r * s, z);
 }
 
@@ -133,25 +154,91 @@ struct RayCtx {
 };
 
 RT_FN f3 motion_shift(const KernelParams& P, int m, float time) {
-  f3 v0 = ld3(P.motions + 8 * m), v1 = ld3(P.motions + 8 * m + 4);
+  f3 v0 = ldc3(cf(P.motions) + 8 * m), v1 = ldc3(cf(P.motions) + 8 * m + 4);
   return (1.0f - time) * v0 + time * v1;
 }
 
 RT_FN float safe_rcp(float d) { return RT_RCP(fabsf(d) > 1e-20f ? d : copysignf(1e-20f, d)); }
 
-// Closest hit within (tmin, tbest) over one BVH; ties go to the smaller depth-first `order`
+// Closest hit so far.  key = (bits of t) << 32 | depth-first order: for t > 0 the integer
+// order of the key is the reference's closest-hit rule — smaller t, ties to the earlier leaf
+// (Geometry.hs:340-361) — so one 64-bit compare replaces the t / tie / validity mask logic.
+// Invalid candidates carry t = NaN (bits above +inf); the initial key is (+inf, 0).
+struct Closest {
+  float t;
+  unsigned long long key;
+  int prim;
+};
+RT_FN Closest no_hit() { return Closest{kInf, 0x7f80000000000000ull, -1}; }
+RT_FN unsigned long long hit_key(float t, int ord) {
+  return ((unsigned long long)(unsigned)RT_F2I(t) << 32) | (unsigned)ord;
+}
+
+// One leaf primitive (Geometry.hs:58-144) against the open interval (tmin, C.t).  Branch-free:
+// each test folds into one validity margin q (valid iff q >= 0), so there is a single select
+// and no per-test lane-mask bookkeeping on the scalar unit.  When `pr` is wave-uniform (flat
+// sets) the record is read with scalar loads and the kind / motion tests are scalar branches.
+RT_FN void test_prim(const KernelParams& P, cfp pr, int pi, const RayCtx& R, float tmin, Closest& C) {
+  RT_COUNT(1);
+  v4 a = ldc4(pr), b = ldc4(pr + 4);
+  const int kf = RT_F2I(a.w);
+  f3 o = R.o;
+  if (kf & RT_FLAG_MOTION) o = o - motion_shift(P, RT_F2I(pr[15]), R.time);
+  const int gid = RT_F2I(b.w);
+  const int ord = RT_F2I(pr[11]);
+  const bool self = gid == R.self_gid;
+  float t, q;
+  if ((kf & RT_KIND_MASK) == 0) {
+    // sphere (Geometry.hs:58-94); geometric discriminant for FP32 robustness.  A ray leaving
+    // this sphere can only reach the far root 2h (the near one is t = 0).
+    f3 oc = xyz(a) - o;
+    float h = dot(R.d, oc);
+    f3 l = oc - h * R.d;
+    float disc = b.y - dot(l, l);
+    float sq = sqrtf(fmaxf(disc, 0.0f));
+    float r1 = h - sq, r2 = h + sq;
+    t = self ? 2.0f * h : (r1 > tmin ? r1 : r2);
+    q = self ? 1.0f : disc;
+  } else {
+    // planeShape (Geometry.hs:117-144); parallelogram a, b in [0,1], triangle a, b >= 0, a + b <= 1
+    f3 n = xyz(a);
+    float denom = dot(n, R.d);
+    f3 qo = xyz(b) - o;
+    t = dot(n, qo) * RT_RCP(denom);
+    v4 c = ldc4(pr + 8), e = ldc4(pr + 12);
+    f3 prel = t * R.d - qo;
+    float aa = dot(prel, xyz(c)), bb = dot(prel, xyz(e));
+    float upper = ((kf & RT_KIND_MASK) == 1) ? fminf(1.0f - aa, 1.0f - bb) : 1.0f - aa - bb;
+    q = fminf(fminf(fminf(aa, bb), upper), fabsf(denom) - 1e-8f);
+    q = self ? -1.0f : q;
+  }
+  const float tc = (q >= 0.0f && t > tmin) ? t : __builtin_nanf("");
+  const unsigned long long key = hit_key(tc, ord);
+  const bool take = key < C.key;
+  C.key = take ? key : C.key;
+  C.t = take ? tc : C.t;
+  C.prim = take ? pi : C.prim;
+}
+
+RT_FN void trace_leaf(const KernelParams& P, cfp prims, int first, int count, const RayCtx& R, float tmin,
+                      Closest& C) {
+  for (int k = 0; k < count; ++k) test_prim(P, prims + 16 * (size_t)(first + k), first + k, R, tmin, C);
+}
+
+// Closest hit within (tmin, C.t) over one BVH; ties go to the smaller depth-first `order`
 // (the reference's group / bvhNode tie-break).  stack[k * stride] is this lane's stack.
-RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmin, float& tbest, int& best,
-                     int& best_order, int* stack, int stride, int* overflow) {
+RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmin, Closest& C, int* stack,
+                     int stride, int* overflow) {
   if (root == RT_EMPTY_ROOT) return;
   int sp = 0;
   int node = root;
   for (;;) {
     if (node >= 0) {
       RT_COUNT(0);
-      const float* nd = P.nodes + 16 * (size_t)node;
-      v4 n0 = ld4(nd), n1 = ld4(nd + 4), n2 = ld4(nd + 8);
-      i4 n3 = *reinterpret_cast<const i4*>(nd + 12);
+      cfp nd = cf(P.nodes) + 16 * (size_t)node;
+      v4 n0 = ldc4(nd), n1 = ldc4(nd + 4), n2 = ldc4(nd + 8);
+      const RT_CAS i4* n3p = (const RT_CAS i4*)(nd + 12);
+      i4 n3 = i4{n3p->x, n3p->y, n3p->z, n3p->w};
       float lx0 = fmaf(n0.x, R.idir.x, -R.oidir.x), lx1 = fmaf(n0.y, R.idir.x, -R.oidir.x);
       float ly0 = fmaf(n0.z, R.idir.y, -R.oidir.y), ly1 = fmaf(n0.w, R.idir.y, -R.oidir.y);
       float lz0 = fmaf(n2.x, R.idir.z, -R.oidir.z), lz1 = fmaf(n2.y, R.idir.z, -R.oidir.z);
@@ -159,9 +246,9 @@ RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmi
       float ry0 = fmaf(n1.z, R.idir.y, -R.oidir.y), ry1 = fmaf(n1.w, R.idir.y, -R.oidir.y);
       float rz0 = fmaf(n2.z, R.idir.z, -R.oidir.z), rz1 = fmaf(n2.w, R.idir.z, -R.oidir.z);
       float lnear = fmaxf(fmaxf(fminf(lx0, lx1), fminf(ly0, ly1)), fmaxf(fminf(lz0, lz1), tmin));
-      float lfar = fminf(fminf(fmaxf(lx0, lx1), fmaxf(ly0, ly1)), fminf(fmaxf(lz0, lz1), tbest));
+      float lfar = fminf(fminf(fmaxf(lx0, lx1), fmaxf(ly0, ly1)), fminf(fmaxf(lz0, lz1), C.t));
       float rnear = fmaxf(fmaxf(fminf(rx0, rx1), fminf(ry0, ry1)), fmaxf(fminf(rz0, rz1), tmin));
-      float rfar = fminf(fminf(fmaxf(rx0, rx1), fmaxf(ry0, ry1)), fminf(fmaxf(rz0, rz1), tbest));
+      float rfar = fminf(fminf(fmaxf(rx0, rx1), fmaxf(ry0, ry1)), fminf(fmaxf(rz0, rz1), C.t));
       bool hl = lnear <= lfar, hr = rnear <= rfar;
       if (hl && hr) {
         int nearc = n3.x, farc = n3.y;
@@ -188,60 +275,27 @@ RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmi
       }
     } else {
       int enc = ~node;
-      int first = enc >> 4, count = (enc & 15) + 1;
-      for (int k = 0; k < count; ++k) {
-        RT_COUNT(1);
-        int pi = first + k;
-        const float* pr = P.prims + 16 * (size_t)pi;
-        v4 a = ld4(pr), b = ld4(pr + 4);
-        int kf = RT_F2I(a.w);
-        f3 o = R.o;
-        if (kf & RT_FLAG_MOTION) o = o - motion_shift(P, RT_F2I(pr[15]), R.time);
-        int gid = RT_F2I(b.w);
-        float t;
-        if ((kf & RT_KIND_MASK) == 0) {
-          // sphere (Geometry.hs:58-94); geometric discriminant for FP32 robustness
-          f3 oc = xyz(a) - o;
-          float h = dot(R.d, oc);
-          if (gid == R.self_gid) {
-            // origin on this sphere: the roots are 0 and 2h, only the far one is reachable
-            t = 2.0f * h;
-          } else {
-            f3 l = oc - h * R.d;
-            float disc = b.y - dot(l, l);
-            if (!(disc >= 0.0f)) continue;
-            float sq = sqrtf(disc);
-            float r1 = h - sq, r2 = h + sq;
-            t = (r1 > tmin) ? r1 : r2;
-          }
-          if (!(t > tmin && t <= tbest && t < kInf)) continue;
-        } else {
-          // planeShape (Geometry.hs:117-144)
-          if (gid == R.self_gid) continue;
-          f3 n = xyz(a);
-          float denom = dot(n, R.d);
-          if (!(fabsf(denom) > 1e-8f)) continue;
-          f3 qo = xyz(b) - o;
-          t = dot(n, qo) * RT_RCP(denom);
-          if (!(t > tmin && t <= tbest && t < kInf)) continue;
-          v4 c = ld4(pr + 8), e = ld4(pr + 12);
-          f3 prel = t * R.d - qo;
-          float aa = dot(prel, xyz(c)), bb = dot(prel, xyz(e));
-          bool inside = ((kf & RT_KIND_MASK) == 1) ? (aa >= 0.0f && aa <= 1.0f && bb >= 0.0f && bb <= 1.0f)
-                                                   : (aa >= 0.0f && bb >= 0.0f && aa + bb <= 1.0f);
-          if (!inside) continue;
-        }
-        int ord = RT_F2I(pr[11]);
-        if (t < tbest || ord < best_order) {
-          tbest = t;
-          best = pi;
-          best_order = ord;
-        }
-      }
+      trace_leaf(P, cf(P.prims), enc >> RT_LEAF_SHIFT, (enc & ((1 << RT_LEAF_SHIFT) - 1)) + 1, R, tmin, C);
     }
     if (sp == 0) break;
     --sp;
     node = stack[sp * stride];
+  }
+}
+
+// Closest hit over one primitive set.  kFlat: the set is a single flat leaf (RT_FLAT_MAX
+// leaves at most): every lane walks the same records in the same order, so the loop is coherent
+// and the records are read with scalar loads (uniform addresses).
+template <bool kFlat>
+RT_FN void closest(const KernelParams& P, cfp prims, int root, const RayCtx& R, float tmin, Closest& C,
+                   int* stack, int stride, int* overflow) {
+  if constexpr (kFlat) {
+    if (root == RT_EMPTY_ROOT) return;
+    const int enc = ~root;  // root comes from the kernel arguments: wave-uniform
+    const int first = enc >> RT_LEAF_SHIFT, count = (enc & ((1 << RT_LEAF_SHIFT) - 1)) + 1;
+    for (int k = 0; k < count; ++k) test_prim(P, prims + 16 * (first + k), first + k, R, tmin, C);
+  } else {
+    trace_set(P, root, R, tmin, C, stack, stride, overflow);
   }
 }
 
@@ -254,9 +308,9 @@ struct HitInfo {
 };
 
 // front side of a boundary hit (constantMedium's case split, Geometry.hs:308)
-RT_FN bool prim_front(const KernelParams& P, int pi, const RayCtx& R, float t) {
-  const float* pr = P.prims + 16 * (size_t)pi;
-  v4 a = ld4(pr);
+RT_FN bool prim_front(const KernelParams& P, cfp prims, int pi, const RayCtx& R, float t) {
+  cfp pr = prims + 16 * (size_t)pi;
+  v4 a = ldc4(pr);
   int kf = RT_F2I(a.w);
   if ((kf & RT_KIND_MASK) == 0) {
     f3 c = xyz(a);
@@ -267,14 +321,14 @@ RT_FN bool prim_front(const KernelParams& P, int pi, const RayCtx& R, float t) {
   return dot(xyz(a), R.d) < 0.0f;
 }
 
-RT_FN HitInfo surface_info(const KernelParams& P, int pi, const RayCtx& R, float t) {
+RT_FN HitInfo surface_info(const KernelParams& P, cfp prims, int pi, const RayCtx& R, float t) {
   HitInfo h;
-  const float* pr = P.prims + 16 * (size_t)pi;
-  v4 a = ld4(pr), b = ld4(pr + 4);
+  cfp pr = prims + 16 * (size_t)pi;
+  v4 a = ldc4(pr), b = ldc4(pr + 4);
   int kf = RT_F2I(a.w);
   h.p = R.o + t * R.d;
   h.gid = RT_F2I(b.w);
-  h.mat = P.prim_mat[pi];
+  h.mat = ldci(P.prim_mat, pi);
   if ((kf & RT_KIND_MASK) == 0) {
     f3 c = xyz(a);
     if (kf & RT_FLAG_MOTION) c = c + motion_shift(P, RT_F2I(pr[15]), R.time);
@@ -284,8 +338,8 @@ RT_FN HitInfo surface_info(const KernelParams& P, int pi, const RayCtx& R, float
     int uvf = RT_F2I(b.z);
     f3 on = outward;
     if (uvf >= 0) {
-      const float* fr = P.uvframes + 12 * uvf;
-      on = mk3(dot(ld3(fr), outward), dot(ld3(fr + 4), outward), dot(ld3(fr + 8), outward));
+      cfp fr = cf(P.uvframes) + 12 * uvf;
+      on = mk3(dot(ldc3(fr), outward), dot(ldc3(fr + 4), outward), dot(ldc3(fr + 8), outward));
     }
     // sphereUV (Geometry.hs:100-104)
     h.u = atan2f(on.x, on.z) * (0.5f / kPi) + 0.5f;
@@ -298,8 +352,8 @@ RT_FN HitInfo surface_info(const KernelParams& P, int pi, const RayCtx& R, float
     f3 o = R.o;
     if (kf & RT_FLAG_MOTION) o = o - motion_shift(P, RT_F2I(pr[15]), R.time);
     f3 prel = (o + t * R.d) - xyz(b);
-    float aa = dot(prel, ld3(pr + 8)), bb = dot(prel, ld3(pr + 12));
-    const float* uv = P.prim_uv + 6 * (size_t)pi;
+    float aa = dot(prel, ldc3(pr + 8)), bb = dot(prel, ldc3(pr + 12));
+    cfp uv = cf(P.prim_uv) + 6 * (size_t)pi;
     float w0 = 1.0f - aa - bb;
     h.u = w0 * uv[0] + aa * uv[2] + bb * uv[4];
     h.v = w0 * uv[1] + aa * uv[3] + bb * uv[5];
@@ -308,12 +362,12 @@ RT_FN HitInfo surface_info(const KernelParams& P, int pi, const RayCtx& R, float
 }
 
 RT_FN f3 eval_texture(const KernelParams& P, int tex, float u, float v) {
-  const DevTexture& T = P.texs[tex];
-  f3 c0 = ld3(T.c0);
-  if (T.kind == 0) return c0;
+  const RT_CAS DevTexture* T = (const RT_CAS DevTexture*)P.texs + tex;
+  f3 c0 = f3{T->c0[0], T->c0[1], T->c0[2]};
+  if (T->kind == 0) return c0;
   // checkerTexture (Texture.hs:45-53)
-  int i = (int)floorf(u * (float)T.nu), j = (int)floorf(v * (float)T.nv);
-  return ((i + j) & 1) == 0 ? c0 : ld3(T.c1);
+  int i = (int)floorf(u * (float)T->nu), j = (int)floorf(v * (float)T->nv);
+  return ((i + j) & 1) == 0 ? c0 : f3{T->c1[0], T->c1[1], T->c1[2]};
 }
 
 // rt_hit of a redirect target: parallelogram on (0, infinity) (Ray.hs:143-145)
@@ -335,13 +389,18 @@ RT_FN long long to_fixed(float x, bool& bad) {
     bad = true;
     return 0;
   }
+#ifdef RT_EXP_CHEAP_FIXED  // ablation: 32-bit conversion only (wrong above 2^31 / 2^16)
+  return (long long)(int)(x * 65536.0f) << 16;
+#else
   return (long long)((double)x * RT_FIX_SCALE);
+#endif
 }
 
 // The persistent lane loop.  `grab(need)` is wave-collective: it returns a fresh item for
 // lanes with need == true.  `commit(tile_pixel, sx, sy, sz, bad)` adds a finished item's sums.
-template <class Grab, class Commit>
-RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, int* stack, int stride) {
+template <bool kFlat, class Grab, class Commit>
+RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, int* stack, int stride, const float* prims_) {
+  const cfp prims = cf(prims_);
   int overflow = 0;
   const int W = P.cam.width, tile_pixels = P.tile_rows * W;
   const int spp = P.cam.spp, max_depth = P.cam.max_depth;
@@ -402,26 +461,26 @@ RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, int* stac
     // ---- closest hit over the surfaces and every medium (Ray.hs:178)
     R.idir = mk3(safe_rcp(R.d.x), safe_rcp(R.d.y), safe_rcp(R.d.z));
     R.oidir = R.o * R.idir;
-    float tbest = kInf;
-    int best = -1, best_order = 0x7fffffff;
-    trace_set(P, P.surface_root, R, kTmin, tbest, best, best_order, stack, stride, &overflow);
+    Closest C = no_hit();
+    closest<kFlat>(P, prims, P.surface_root, R, kTmin, C, stack, stride, &overflow);
+    float tbest = C.t;
+    const int best = C.prim;
     int hit_medium = -1;
     for (int m = 0; m < P.n_media; ++m) {
       // constantMedium (Geometry.hs:306-328)
       const DevMedium& M = P.media[m];
-      float t1 = kInf;
-      int b1 = -1, o1 = 0x7fffffff;
-      trace_set(P, M.root, R, kTmin, t1, b1, o1, stack, stride, &overflow);
-      if (b1 < 0) continue;
+      Closest C1 = no_hit();
+      closest<kFlat>(P, prims, M.root, R, kTmin, C1, stack, stride, &overflow);
+      if (C1.prim < 0) continue;
+      const float t1 = C1.t;
       float lo, hi;
-      if (prim_front(P, b1, R, t1)) {
+      if (prim_front(P, prims, C1.prim, R, t1)) {
         if (!(t1 < tbest)) continue;
-        float t2 = kInf;
-        int b2 = -1, o2 = 0x7fffffff;
-        trace_set(P, M.root, R, t1, t2, b2, o2, stack, stride, &overflow);
-        if (b2 < 0) continue;
+        Closest C2 = no_hit();
+        closest<kFlat>(P, prims, M.root, R, t1, C2, stack, stride, &overflow);
+        if (C2.prim < 0) continue;
         lo = t1;
-        hi = t2;
+        hi = C2.t;
       } else {
         lo = kTmin;
         hi = t1;
@@ -459,9 +518,10 @@ RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, int* stac
         h.mat = P.media[hit_medium].material;
         h.gid = -1;
       } else {
-        h = surface_info(P, best, R, tbest);
+        h = surface_info(P, prims, best, R, tbest);
       }
-      const DevMaterial& Mt = P.mats[h.mat];
+      const RT_CAS DevMaterial* Mp = (const RT_CAS DevMaterial*)P.mats + h.mat;
+      const DevMaterial Mt = DevMaterial{Mp->kind, Mp->tex, Mp->param, 0};
       u4 w = philox(pix, (uint32_t)sample, (uint32_t)seg, RT_EV_SCATTER, P.key0, P.key1);
       const bool last = seg + 1 >= max_depth;  // rayColor (depth - 1) with depth - 1 <= 0 is zero
       f3 newdir = R.d;

@@ -45,11 +45,14 @@ struct Commit {
 
 void* worker(void* arg) {
   Shared* s = (Shared*)arg;
-  std::vector<int> stack(s->P->stack_depth);
+  std::vector<int> stack(s->P->stack_depth + 1);
   for (auto& c : rt_emu::counters) c = 0;
   Grab g{s};
   Commit c{s};
-  if (rtk::lane_loop(*s->P, g, c, stack.data(), 1)) s->overflow = 1;
+  const bool flat = s->P->stack_depth == 0;  // the emulator marks flat scenes with depth 0
+  if (flat ? rtk::lane_loop<true>(*s->P, g, c, nullptr, 0, s->P->prims)
+           : rtk::lane_loop<false>(*s->P, g, c, stack.data(), 1, s->P->prims))
+    s->overflow = 1;
   for (int i = 0; i < 4; ++i) s->cnt[i] += rt_emu::counters[i];
   return nullptr;
 }
@@ -79,7 +82,8 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
   P.surface_root = H.surface_root;
   P.n_media = H.n_media;
   for (int k = 0; k < H.n_media; ++k) P.media[k] = H.media[k];
-  P.stack_depth = H.max_depth > 1 ? H.max_depth : 1;
+  P.stack_depth = H.flat ? 0 : (H.max_depth > 1 ? H.max_depth : 1);
+  P.n_prims = H.n_prims;
   rt_host_plan_work(P, 4096);
   if (chunk > 0) {
     P.chunk = chunk;
