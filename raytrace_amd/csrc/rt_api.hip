@@ -58,6 +58,7 @@ struct rt_device_scene {
   int surface_root = RT_EMPTY_ROOT;
   int n_media = 0;
   DevMedium media[RT_MAX_MEDIA];
+  DevFlatSet flat_sets[1 + RT_MAX_MEDIA];
   int n_nodes = 0, n_prims = 0, max_depth = 0;
   int stack_depth = 1;       // LDS stack entries per lane
   bool flat = false;         // all sets are flat leaves: the LDS-resident variant
@@ -130,6 +131,7 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
   s->surface_root = H.surface_root;
   s->n_media = H.n_media;
   for (int k = 0; k < H.n_media; ++k) s->media[k] = H.media[k];
+  for (int k = 0; k <= RT_MAX_MEDIA; ++k) s->flat_sets[k] = H.flat_sets[k];
   s->n_nodes = H.n_nodes;
   s->n_prims = H.n_prims;
   s->max_depth = H.max_depth;
@@ -175,6 +177,7 @@ int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint
   P.surface_root = s->surface_root;
   P.n_media = s->n_media;
   for (int k = 0; k < s->n_media; ++k) P.media[k] = s->media[k];
+  for (int k = 0; k <= RT_MAX_MEDIA; ++k) P.flat_sets[k] = s->flat_sets[k];
   P.stack_depth = s->stack_depth;
   P.n_prims = s->n_prims;
   rt_host_plan_work(P, (long long)s->resident_blocks * RT_BLOCK);

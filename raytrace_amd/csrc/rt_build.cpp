@@ -6,6 +6,7 @@
 //    b = nS.(u x (p-q)) = (p-q).wb) in binary64 and rounds it once to FP32,
 //  * builds one BVH per primitive set (surfaces, then each medium's boundary),
 //  * evaluates the camera set-up of Ray.hs:122-155 in binary64, in the reference's order.
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -155,7 +156,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
 
   // one BVH per set; primitives stored in leaf order, set after set
   std::vector<int> order;
-  std::vector<int> roots(n_sets);
+  std::vector<int> roots(n_sets), set_begin(n_sets + 1, 0);
   S.nodes.clear();
   S.max_depth = 0;
   for (int s = 0; s < n_sets; ++s) {
@@ -165,10 +166,34 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     order.insert(order.end(), bo.order.begin(), bo.order.end());
     roots[s] = bo.root;
     S.max_depth = std::max(S.max_depth, bo.max_depth);
+    set_begin[s + 1] = (int)order.size();
   }
   if (S.max_depth > RT_STACK_DEPTH)
     return fail(err, RT_E_STACK, "BVH depth %d exceeds the traversal stack (%d)", S.max_depth, RT_STACK_DEPTH);
   const int n = (int)order.size();
+  S.flat = S.nodes.empty() && n <= RT_LDS_PRIMS_MAX;
+  if (S.flat) {
+    // group each set's single leaf by class (rt_internal.h DevFlatSet); stable within a class
+    auto cls = [&](int i) {
+      const rt_prim& p = sc->prims[i];
+      if (p.motion >= 0) return 3;
+      return p.kind == RT_PRIM_PARALLELOGRAM ? 0 : p.kind == RT_PRIM_TRIANGLE ? 1 : 2;
+    };
+    for (int s = 0; s < n_sets; ++s) {
+      int* b = order.data() + set_begin[s];
+      int* e = order.data() + set_begin[s + 1];
+      std::stable_sort(b, e, [&](int x, int y) { return cls(x) < cls(y); });
+      int cnt[4] = {0, 0, 0, 0};
+      for (int* it = b; it != e; ++it) cnt[cls(*it)]++;
+      DevFlatSet& F = S.flat_sets[s];
+      F.first = set_begin[s];
+      F.end_quad = F.first + cnt[0];
+      F.end_tri = F.end_quad + cnt[1];
+      F.end_sphere = F.end_tri + cnt[2];
+      F.end = F.end_sphere + cnt[3];
+      F.pad[0] = F.pad[1] = F.pad[2] = 0;
+    }
+  }
   S.prims.assign((size_t)n * 16, 0.0f);
   S.prim_mat.assign(n, -1);
   S.prim_uv.assign((size_t)n * 6, 0.0f);
@@ -240,7 +265,6 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   }
   S.n_nodes = (int)(S.nodes.size() / 16);
   S.n_prims = n;
-  S.flat = S.n_nodes == 0 && n <= RT_LDS_PRIMS_MAX;
   return RT_OK;
 }
 

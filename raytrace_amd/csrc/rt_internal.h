@@ -62,6 +62,19 @@ struct DevMedium {
   int pad;
 };
 
+// Flat scenes (every set one leaf): a set's primitives are grouped by class so the kernel runs
+// one specialised, branch-free loop per class: [first, end_quad) static parallelograms,
+// [end_quad, end_tri) static triangles, [end_tri, end_sphere) static spheres,
+// [end_sphere, end) moving primitives of any kind.  The closest-hit tie-break uses each record's
+// depth-first `order`, so the test order within a set does not matter.
+#define RT_PRIM_CLASS_QUAD 1
+#define RT_PRIM_CLASS_TRI 2
+#define RT_PRIM_CLASS_SPHERE 0
+struct DevFlatSet {
+  int first, end_quad, end_tri, end_sphere, end;
+  int pad[3];
+};
+
 struct DevTarget {
   float q[3], u[3], v[3];
   float n[3];     // unit normal of u x v
@@ -105,6 +118,7 @@ struct KernelParams {
   int n_targets;
   float rem_prob;
   DevMedium media[RT_MAX_MEDIA];
+  DevFlatSet flat_sets[1 + RT_MAX_MEDIA];  // flat kernel: set 0 = surfaces, set m + 1 = medium m
   DevTarget targets[RT_MAX_TARGETS];
   DevCamera cam;
   uint32_t key0, key1;
@@ -122,6 +136,7 @@ struct HostScene {
   int surface_root = RT_EMPTY_ROOT;
   int n_media = 0;
   DevMedium media[RT_MAX_MEDIA];
+  DevFlatSet flat_sets[1 + RT_MAX_MEDIA] = {};
   int n_nodes = 0, n_prims = 0, max_depth = 0;
   bool flat = false;  // every set is a single flat leaf (no BVH nodes)
 };

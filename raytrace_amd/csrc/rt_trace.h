@@ -49,6 +49,7 @@ extern thread_local long long counters[4];
 #define RT_LOG(x) logf(x)
 #define RT_RSQRT(x) (1.0f / sqrtf(x))
 #define RT_RCP(x) (1.0f / (x))
+#define RT_SQRT(x) sqrtf(x)
 #define RT_COUNT(i) (++rt_emu::counters[i])
 #define RT_CAS
 #else
@@ -59,11 +60,20 @@ extern thread_local long long counters[4];
 #define RT_LOG(x) __logf(x)
 #define RT_RSQRT(x) __frsqrt_rn(x)
 #define RT_RCP(x) __builtin_amdgcn_rcpf(x)
+#define RT_SQRT(x) __builtin_amdgcn_sqrtf(x)  // v_sqrt_f32 (1 ulp), no IEEE fix-up sequence
 #define RT_COUNT(i) ((void)0)
 // Scene data is read through the constant address space: the kernel never writes it, so
 // wave-uniform reads (flat sets, kernel-argument indices) become scalar loads into SGPRs and
 // divergent reads stay vector loads.
 #define RT_CAS __attribute__((address_space(4)))
+#endif
+
+// Debug hooks (no-ops; the emulator's debug build defines them to trace one path on the CPU)
+#ifndef RT_HOOK_SEGMENT
+#define RT_HOOK_SEGMENT(pix, sample, seg, R, tbest, best, hit_medium, L, T)
+#endif
+#ifndef RT_HOOK_SAMPLE
+#define RT_HOOK_SAMPLE(pix, sample, L)
 #endif
 
 namespace rtk {
@@ -94,6 +104,13 @@ RT_FN f3 normalize(f3 v) {
   if (l <= 1e-12f) return v;  // linear's normalize leaves (near-)zero vectors alone
   return RT_RSQRT(l) * v;
 }
+// Re-normalise a direction that is unit in exact arithmetic (reflect / refract of unit vectors,
+// Core.hs:49-51, Material.hs:81-85).  The reference's sphere test assumes |d| = 1 (Geometry.hs:
+// 64-68); in binary64 the rounding drift is ~1e-16 and harmless, but in FP32 a chain of total
+// internal reflections inside a glass sphere amplifies it each bounce (the point lands off the
+// surface, the normal (p - c) / r is no longer unit, reflect lengthens d) until the path
+// diverges.  Re-normalising keeps the FP32 path on the exact-arithmetic result.
+RT_FN f3 unit(f3 v) { return RT_RSQRT(dot(v, v)) * v; }
 RT_FN f3 reflect(f3 n, f3 v) { return v - (2.0f * dot(n, v)) * n; }  // Core.hs:49-51
 RT_FN f3 xyz(v4 v) { return f3{v.x, v.y, v.z}; }
 RT_FN v4 ld4(const float* p) { return *reinterpret_cast<const v4*>(p); }
@@ -174,50 +191,83 @@ RT_FN unsigned long long hit_key(float t, int ord) {
   return ((unsigned long long)(unsigned)RT_F2I(t) << 32) | (unsigned)ord;
 }
 
-// One leaf primitive (Geometry.hs:58-144) against the open interval (tmin, C.t).  Branch-free:
-// each test folds into one validity margin q (valid iff q >= 0), so there is a single select
-// and no per-test lane-mask bookkeeping on the scalar unit.  When `pr` is wave-uniform (flat
-// sets) the record is read with scalar loads and the kind / motion tests are scalar branches.
-RT_FN void test_prim(const KernelParams& P, cfp pr, int pi, const RayCtx& R, float tmin, Closest& C) {
-  RT_COUNT(1);
-  v4 a = ldc4(pr), b = ldc4(pr + 4);
-  const int kf = RT_F2I(a.w);
-  f3 o = R.o;
-  if (kf & RT_FLAG_MOTION) o = o - motion_shift(P, RT_F2I(pr[15]), R.time);
-  const int gid = RT_F2I(b.w);
-  const int ord = RT_F2I(pr[11]);
-  const bool self = gid == R.self_gid;
-  float t, q;
-  if ((kf & RT_KIND_MASK) == 0) {
-    // sphere (Geometry.hs:58-94); geometric discriminant for FP32 robustness.  A ray leaving
-    // this sphere can only reach the far root 2h (the near one is t = 0).
-    f3 oc = xyz(a) - o;
-    float h = dot(R.d, oc);
-    f3 l = oc - h * R.d;
-    float disc = b.y - dot(l, l);
-    float sq = sqrtf(fmaxf(disc, 0.0f));
-    float r1 = h - sq, r2 = h + sq;
-    t = self ? 2.0f * h : (r1 > tmin ? r1 : r2);
-    q = self ? 1.0f : disc;
-  } else {
-    // planeShape (Geometry.hs:117-144); parallelogram a, b in [0,1], triangle a, b >= 0, a + b <= 1
-    f3 n = xyz(a);
-    float denom = dot(n, R.d);
-    f3 qo = xyz(b) - o;
-    t = dot(n, qo) * RT_RCP(denom);
-    v4 c = ldc4(pr + 8), e = ldc4(pr + 12);
-    f3 prel = t * R.d - qo;
-    float aa = dot(prel, xyz(c)), bb = dot(prel, xyz(e));
-    float upper = ((kf & RT_KIND_MASK) == 1) ? fminf(1.0f - aa, 1.0f - bb) : 1.0f - aa - bb;
-    q = fminf(fminf(fminf(aa, bb), upper), fabsf(denom) - 1e-8f);
-    q = self ? -1.0f : q;
-  }
+// A primitive record (rt_internal.h layout, 64 B): a = (center | normal, kind+flags),
+// b = (radius, r^2, uvframe, gid | q, gid), c = (-, -, -, order | wa, order), e = (wb, motion).
+struct PrimRec {
+  v4 a, b, c, e;
+};
+RT_FN PrimRec ld_rec(cfp pr) { return PrimRec{ldc4(pr), ldc4(pr + 4), ldc4(pr + 8), ldc4(pr + 12)}; }
+
+// Primitive intersection (Geometry.hs:58-144), branch-free: each test yields a parameter t and
+// one validity margin q (valid iff q >= 0), so the closest-hit update is a single select with
+// no per-test lane-mask bookkeeping on the scalar unit.
+// sphere (Geometry.hs:58-94); geometric discriminant for FP32 robustness.  A ray leaving this
+// sphere (self) can only reach the far root 2h (the near one is t = 0).
+RT_FN void isect_sphere(const PrimRec& r, f3 o, const RayCtx& R, float tmin, bool self, float& t, float& q) {
+  f3 oc = xyz(r.a) - o;
+  float h = dot(R.d, oc);
+  f3 l = oc - h * R.d;
+  float disc = r.b.y - dot(l, l);
+  float sq = RT_SQRT(fmaxf(disc, 0.0f));
+  float r1 = h - sq, r2 = h + sq;
+  float tn = r1 > tmin ? r1 : r2;
+  t = self ? 2.0f * h : tn;
+  q = self ? 1.0f : disc;
+}
+// planeShape (Geometry.hs:117-144): parallelogram a, b in [0,1]; triangle a, b >= 0, a + b <= 1
+template <bool kQuad>
+RT_FN void isect_plane(const PrimRec& r, f3 o, const RayCtx& R, bool self, float& t, float& q) {
+  f3 n = xyz(r.a);
+  float denom = dot(n, R.d);
+  f3 qo = xyz(r.b) - o;
+  t = dot(n, qo) * RT_RCP(denom);
+  f3 prel = t * R.d - qo;
+  float aa = dot(prel, xyz(r.c)), bb = dot(prel, xyz(r.e));
+  float upper = kQuad ? fminf(1.0f - aa, 1.0f - bb) : 1.0f - aa - bb;
+  q = fminf(fminf(fminf(aa, bb), upper), fabsf(denom) - 1e-8f);
+  q = self ? -1.0f : q;
+}
+RT_FN void consider(Closest& C, float t, float q, float tmin, int ord, int pi) {
   const float tc = (q >= 0.0f && t > tmin) ? t : __builtin_nanf("");
   const unsigned long long key = hit_key(tc, ord);
   const bool take = key < C.key;
   C.key = take ? key : C.key;
   C.t = take ? tc : C.t;
   C.prim = take ? pi : C.prim;
+}
+
+// Any primitive record against the open interval (tmin, C.t).  When the record is wave-uniform
+// (flat sets) it sits in SGPRs and the kind / motion tests are scalar branches.
+RT_FN void test_rec(const KernelParams& P, const PrimRec& r, int pi, const RayCtx& R, float tmin, Closest& C) {
+  RT_COUNT(1);
+  const int kf = RT_F2I(r.a.w);
+  f3 o = R.o;
+  if (kf & RT_FLAG_MOTION) o = o - motion_shift(P, RT_F2I(r.e.w), R.time);
+  const bool self = RT_F2I(r.b.w) == R.self_gid;
+  float t, q;
+  if ((kf & RT_KIND_MASK) == 0)
+    isect_sphere(r, o, R, tmin, self, t, q);
+  else if ((kf & RT_KIND_MASK) == 1)
+    isect_plane<true>(r, o, R, self, t, q);
+  else
+    isect_plane<false>(r, o, R, self, t, q);
+  consider(C, t, q, tmin, RT_F2I(r.c.w), pi);
+}
+
+// A static primitive of a known kind (flat sets are grouped by class: rt_build.cpp).
+template <int kKind>
+RT_FN void test_static(const PrimRec& r, int pi, const RayCtx& R, float tmin, Closest& C) {
+  RT_COUNT(1);
+  const bool self = RT_F2I(r.b.w) == R.self_gid;
+  float t, q;
+  if constexpr (kKind == RT_PRIM_CLASS_SPHERE)
+    isect_sphere(r, R.o, R, tmin, self, t, q);
+  else
+    isect_plane<kKind == RT_PRIM_CLASS_QUAD>(r, R.o, R, self, t, q);
+  consider(C, t, q, tmin, RT_F2I(r.c.w), pi);
+}
+RT_FN void test_prim(const KernelParams& P, cfp pr, int pi, const RayCtx& R, float tmin, Closest& C) {
+  test_rec(P, ld_rec(pr), pi, R, tmin, C);
 }
 
 RT_FN void trace_leaf(const KernelParams& P, cfp prims, int first, int count, const RayCtx& R, float tmin,
@@ -287,14 +337,18 @@ RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmi
 // leaves at most): every lane walks the same records in the same order, so the loop is coherent
 // and the records are read with scalar loads (uniform addresses).
 template <bool kFlat>
-RT_FN void closest(const KernelParams& P, cfp prims, int root, const RayCtx& R, float tmin, Closest& C,
+RT_FN void closest(const KernelParams& P, cfp prims, int root, int set, const RayCtx& R, float tmin, Closest& C,
                    int* stack, int stride, int* overflow) {
   if constexpr (kFlat) {
-    if (root == RT_EMPTY_ROOT) return;
-    const int enc = ~root;  // root comes from the kernel arguments: wave-uniform
-    const int first = enc >> RT_LEAF_SHIFT, count = (enc & ((1 << RT_LEAF_SHIFT) - 1)) + 1;
-    for (int k = 0; k < count; ++k) test_prim(P, prims + 16 * (first + k), first + k, R, tmin, C);
+    // set comes from the kernel arguments: the ranges are wave-uniform, every loop is scalar
+    const DevFlatSet& S = P.flat_sets[set];
+    int k = S.first;
+    for (; k < S.end_quad; ++k) test_static<RT_PRIM_CLASS_QUAD>(ld_rec(prims + 16 * k), k, R, tmin, C);
+    for (; k < S.end_tri; ++k) test_static<RT_PRIM_CLASS_TRI>(ld_rec(prims + 16 * k), k, R, tmin, C);
+    for (; k < S.end_sphere; ++k) test_static<RT_PRIM_CLASS_SPHERE>(ld_rec(prims + 16 * k), k, R, tmin, C);
+    for (; k < S.end; ++k) test_rec(P, ld_rec(prims + 16 * k), k, R, tmin, C);
   } else {
+    (void)set;
     trace_set(P, root, R, tmin, C, stack, stride, overflow);
   }
 }
@@ -462,7 +516,7 @@ RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, int* stac
     R.idir = mk3(safe_rcp(R.d.x), safe_rcp(R.d.y), safe_rcp(R.d.z));
     R.oidir = R.o * R.idir;
     Closest C = no_hit();
-    closest<kFlat>(P, prims, P.surface_root, R, kTmin, C, stack, stride, &overflow);
+    closest<kFlat>(P, prims, P.surface_root, 0, R, kTmin, C, stack, stride, &overflow);
     float tbest = C.t;
     const int best = C.prim;
     int hit_medium = -1;
@@ -470,14 +524,14 @@ RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, int* stac
       // constantMedium (Geometry.hs:306-328)
       const DevMedium& M = P.media[m];
       Closest C1 = no_hit();
-      closest<kFlat>(P, prims, M.root, R, kTmin, C1, stack, stride, &overflow);
+      closest<kFlat>(P, prims, M.root, m + 1, R, kTmin, C1, stack, stride, &overflow);
       if (C1.prim < 0) continue;
       const float t1 = C1.t;
       float lo, hi;
       if (prim_front(P, prims, C1.prim, R, t1)) {
         if (!(t1 < tbest)) continue;
         Closest C2 = no_hit();
-        closest<kFlat>(P, prims, M.root, R, t1, C2, stack, stride, &overflow);
+        closest<kFlat>(P, prims, M.root, m + 1, R, t1, C2, stack, stride, &overflow);
         if (C2.prim < 0) continue;
         lo = t1;
         hi = C2.t;
@@ -497,6 +551,7 @@ RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, int* stac
         }
       }
     }
+    RT_HOOK_SEGMENT(pix, sample, seg, R, tbest, best, hit_medium, L, T);
     bool terminate = false;
     if (hit_medium < 0 && best < 0) {
       // miss: cs_background (Ray.hs:179)
@@ -535,7 +590,7 @@ RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, int* stac
           break;
         case 4:  // mirror
           T = T * eval_texture(P, Mt.tex, h.u, h.v);
-          newdir = reflect(h.n, R.d);
+          newdir = unit(reflect(h.n, R.d));
           break;
         case 5: {  // metal
           f3 d2 = reflect(h.n, R.d) + Mt.param * unit_vector(w.y, w.z);
@@ -557,10 +612,10 @@ RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, int* stac
           float x1 = 1.0f - cos_t, x2 = x1 * x1;
           float reflectance = r0 + (1.0f - r0) * (x2 * x2 * x1);
           if (ratio * sin_t > 1.0f || u01(w.x) < reflectance) {
-            newdir = reflect(h.n, R.d);
+            newdir = unit(reflect(h.n, R.d));
           } else {
             f3 perp = ratio * (R.d + cos_t * h.n);
-            newdir = perp - sqrtf(fabsf(1.0f - dot(perp, perp))) * h.n;
+            newdir = unit(perp - sqrtf(fabsf(1.0f - dot(perp, perp))) * h.n);
           }
           break;
         }
@@ -624,6 +679,7 @@ RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, int* stac
       }
     }
     if (terminate) {
+      RT_HOOK_SAMPLE(pix, sample, L);
       sx += to_fixed(L.x, bad);
       sy += to_fixed(L.y, bad);
       sz += to_fixed(L.z, bad);

@@ -82,6 +82,7 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
   P.surface_root = H.surface_root;
   P.n_media = H.n_media;
   for (int k = 0; k < H.n_media; ++k) P.media[k] = H.media[k];
+  for (int k = 0; k <= RT_MAX_MEDIA; ++k) P.flat_sets[k] = H.flat_sets[k];
   P.stack_depth = H.flat ? 0 : (H.max_depth > 1 ? H.max_depth : 1);
   P.n_prims = H.n_prims;
   rt_host_plan_work(P, 4096);

@@ -93,6 +93,17 @@ def test_pawn_demo_matches_published_render(gpu, golden_stats):
     assert np.sqrt(((block8(lin) - gold) ** 2).mean()) < 0.02
 
 
+def test_full_demo1_is_finite(gpu):
+    """demo1 at its full 1200x675x500: long total-internal-reflection chains inside the glass
+    spheres stay finite (directions re-normalised after reflect / refract, rt_trace.h `unit`)."""
+    cs, world, seed = scenes.demo1()
+    img = R.raytrace(cs, world, seed)
+    assert img.shape == (675, 1200, 3)
+    assert np.isfinite(img).all()
+    m = img.reshape(-1, 3).mean(0)
+    assert (m > 0.3).all() and (m < 1.0).all()
+
+
 def test_deterministic_and_shard_invariant(gpu):
     from raytrace_amd.ray import assemble_shards, render_shard
     cs, world, seed = scenes.cornell_box(spp=4, width=50)
