@@ -54,6 +54,7 @@ struct rt_device_scene {
   DevTexture* texs = nullptr;
   float* motions = nullptr;
   float* uvframes = nullptr;
+  int* flat_prim = nullptr;
   int* status = nullptr;
   int surface_root = RT_EMPTY_ROOT;
   int n_media = 0;
@@ -101,6 +102,7 @@ int rt_scene_destroy(rt_device_scene* s) {
   (void)hipFree(s->texs);
   (void)hipFree(s->motions);
   (void)hipFree(s->uvframes);
+  (void)hipFree(s->flat_prim);
   (void)hipFree(s->status);
   delete s;
   return RT_OK;
@@ -124,7 +126,8 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
   if ((rc = upload(&s->nodes, H.nodes)) || (rc = upload(&s->prims, H.prims)) ||
       (rc = upload(&s->prim_mat, H.prim_mat)) || (rc = upload(&s->prim_uv, H.prim_uv)) ||
       (rc = upload(&s->mats, H.mats)) || (rc = upload(&s->texs, H.texs)) || (rc = upload(&s->motions, H.motions)) ||
-      (rc = upload(&s->uvframes, H.uvframes)) || (rc = upload(&s->status, status))) {
+      (rc = upload(&s->uvframes, H.uvframes)) || (rc = upload(&s->flat_prim, H.flat_prim)) ||
+      (rc = upload(&s->status, status))) {
     rt_scene_destroy(s);
     return rc;
   }
@@ -172,6 +175,7 @@ int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint
   P.texs = s->texs;
   P.motions = s->motions;
   P.uvframes = s->uvframes;
+  P.flat_prim = s->flat_prim;
   P.status = s->status;
   P.out = d_out_rgb;
   P.surface_root = s->surface_root;

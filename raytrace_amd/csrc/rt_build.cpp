@@ -194,6 +194,21 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
       F.pad[0] = F.pad[1] = F.pad[2] = 0;
     }
   }
+  // flat scenes: slot of each primitive (rank of its order within the set) and slot -> index
+  std::vector<int> slot_of(n, 0);
+  if (S.flat) {
+    S.flat_prim.assign(n, 0);
+    for (int s = 0; s < n_sets; ++s) {
+      std::vector<int> pos;
+      for (int j = set_begin[s]; j < set_begin[s + 1]; ++j) pos.push_back(j);
+      std::stable_sort(pos.begin(), pos.end(),
+                       [&](int x, int y) { return sc->prims[order[x]].order < sc->prims[order[y]].order; });
+      for (size_t r = 0; r < pos.size(); ++r) {
+        slot_of[pos[r]] = set_begin[s] + (int)r;
+        S.flat_prim[set_begin[s] + r] = pos[r];
+      }
+    }
+  }
   S.prims.assign((size_t)n * 16, 0.0f);
   S.prim_mat.assign(n, -1);
   S.prim_uv.assign((size_t)n * 6, 0.0f);
@@ -223,7 +238,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     }
     f[3] = ibits(kf);
     f[7] = ibits(p.gid);
-    f[11] = ibits(p.order);
+    f[11] = ibits(S.flat ? slot_of[j] : p.order);
     f[15] = ibits(p.motion);
     S.prim_mat[j] = p.set == 0 ? p.material : -1;
   }

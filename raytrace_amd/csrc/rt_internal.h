@@ -65,8 +65,10 @@ struct DevMedium {
 // Flat scenes (every set one leaf): a set's primitives are grouped by class so the kernel runs
 // one specialised, branch-free loop per class: [first, end_quad) static parallelograms,
 // [end_quad, end_tri) static triangles, [end_tri, end_sphere) static spheres,
-// [end_sphere, end) moving primitives of any kind.  The closest-hit tie-break uses each record's
-// depth-first `order`, so the test order within a set does not matter.
+// [end_sphere, end) moving primitives of any kind.  Each record's order word holds its SLOT:
+// set first + rank of its depth-first `order` within the set, so the 64-bit closest-hit key
+// (t, slot) keeps the reference's tie-break whatever the test order, and the winner's index is
+// one lookup, flat_prim[slot], after the loop (the loop itself only tracks the key).
 #define RT_PRIM_CLASS_QUAD 1
 #define RT_PRIM_CLASS_TRI 2
 #define RT_PRIM_CLASS_SPHERE 0
@@ -102,6 +104,7 @@ struct KernelParams {
   const DevTexture* texs;
   const float* motions;    // 8 floats per motion: v0.xyz, -, v1.xyz, -
   const float* uvframes;   // 12 floats per frame: rows of R (xyz, -)
+  const int* flat_prim;    // flat scenes: closest-hit slot -> primitive index (DevFlatSet)
   float* out;
   int* status;             // device word: nonzero on stack overflow
   // persistent-lane work queue (rt_trace.h lane_loop): items = n_chunks x tile pixels
@@ -131,6 +134,7 @@ struct KernelParams {
 struct HostScene {
   std::vector<float> nodes, prims, prim_uv, motions, uvframes;
   std::vector<int> prim_mat;
+  std::vector<int> flat_prim;  // flat scenes: slot -> primitive index
   std::vector<DevMaterial> mats;
   std::vector<DevTexture> texs;
   int surface_root = RT_EMPTY_ROOT;

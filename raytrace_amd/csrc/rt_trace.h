@@ -34,7 +34,6 @@
 #include <cstring>
 #define RT_FN static inline
 namespace rt_emu {
-inline uint32_t umulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 inline int f2i(float f) {
   int i;
   std::memcpy(&i, &f, 4);
@@ -43,7 +42,6 @@ inline int f2i(float f) {
 // traversal counters of the host build (nodes visited, primitives tested, segments)
 extern thread_local long long counters[4];
 }  // namespace rt_emu
-#define RT_UMULHI(a, b) rt_emu::umulhi(a, b)
 #define RT_F2I(f) rt_emu::f2i(f)
 #define RT_SINCOS(x, s, c) (*(s) = sinf(x), *(c) = cosf(x))
 #define RT_LOG(x) logf(x)
@@ -54,7 +52,6 @@ extern thread_local long long counters[4];
 #define RT_CAS
 #else
 #define RT_FN __device__ __forceinline__
-#define RT_UMULHI(a, b) __umulhi(a, b)
 #define RT_F2I(f) __float_as_int(f)
 #define RT_SINCOS(x, s, c) __sincosf(x, s, c)
 #define RT_LOG(x) __logf(x)
@@ -137,8 +134,10 @@ RT_FN u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
       k0 += 0x9E3779B9u;
       k1 += 0xBB67AE85u;
     }
-    uint32_t hi0 = RT_UMULHI(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-    uint32_t hi1 = RT_UMULHI(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    // one full 32x32->64 product per word: a single v_mad_u64_u32 instead of mul_hi + mul_lo
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
     uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
     c0 = n0;
     c1 = lo1;
@@ -197,13 +196,24 @@ struct PrimRec {
   v4 a, b, c, e;
 };
 RT_FN PrimRec ld_rec(cfp pr) { return PrimRec{ldc4(pr), ldc4(pr + 4), ldc4(pr + 8), ldc4(pr + 12)}; }
+struct alignas(64) PrimRec64 {
+  float f[16];
+};
+RT_FN PrimRec ld_rec64(const RT_CAS PrimRec64* p) {
+  const RT_CAS float* r = p->f;
+  return PrimRec{v4{r[0], r[1], r[2], r[3]}, v4{r[4], r[5], r[6], r[7]}, v4{r[8], r[9], r[10], r[11]},
+                 v4{r[12], r[13], r[14], r[15]}};
+}
 
 // Primitive intersection (Geometry.hs:58-144), branch-free: each test yields a parameter t and
-// one validity margin q (valid iff q >= 0), so the closest-hit update is a single select with
-// no per-test lane-mask bookkeeping on the scalar unit.
+// one validity margin q (valid iff q >= 0) that also carries the interval test t > tmin as
+// t - up(tmin) >= 0 (up = next float: exact for the open interval), so the closest-hit update is
+// a single compare and select with no per-test lane-mask bookkeeping on the scalar unit.
+RT_FN float float_up(float x) { return __builtin_bit_cast(float, RT_F2I(x) + 1); }  // x > 0
 // sphere (Geometry.hs:58-94); geometric discriminant for FP32 robustness.  A ray leaving this
 // sphere (self) can only reach the far root 2h (the near one is t = 0).
-RT_FN void isect_sphere(const PrimRec& r, f3 o, const RayCtx& R, float tmin, bool self, float& t, float& q) {
+RT_FN void isect_sphere(const PrimRec& r, f3 o, const RayCtx& R, float tmin, float tmin_up, bool self, float& t,
+                        float& q) {
   f3 oc = xyz(r.a) - o;
   float h = dot(R.d, oc);
   f3 l = oc - h * R.d;
@@ -212,33 +222,40 @@ RT_FN void isect_sphere(const PrimRec& r, f3 o, const RayCtx& R, float tmin, boo
   float r1 = h - sq, r2 = h + sq;
   float tn = r1 > tmin ? r1 : r2;
   t = self ? 2.0f * h : tn;
-  q = self ? 1.0f : disc;
+  q = fminf(self ? 1.0f : disc, t - tmin_up);
 }
 // planeShape (Geometry.hs:117-144): parallelogram a, b in [0,1]; triangle a, b >= 0, a + b <= 1
 template <bool kQuad>
-RT_FN void isect_plane(const PrimRec& r, f3 o, const RayCtx& R, bool self, float& t, float& q) {
+RT_FN void isect_plane(const PrimRec& r, f3 o, const RayCtx& R, float tmin_up, bool self, float& t, float& q) {
   f3 n = xyz(r.a);
   float denom = dot(n, R.d);
   f3 qo = xyz(r.b) - o;
   t = dot(n, qo) * RT_RCP(denom);
   f3 prel = t * R.d - qo;
   float aa = dot(prel, xyz(r.c)), bb = dot(prel, xyz(r.e));
-  float upper = kQuad ? fminf(1.0f - aa, 1.0f - bb) : 1.0f - aa - bb;
-  q = fminf(fminf(fminf(aa, bb), upper), fabsf(denom) - 1e-8f);
-  q = self ? -1.0f : q;
+  float m1 = kQuad ? fminf(fminf(aa, bb), 1.0f - aa) : fminf(fminf(aa, bb), 1.0f - aa - bb);
+  float m2 = fminf(fabsf(denom) - 1e-8f, t - tmin_up);
+  if (kQuad) m2 = fminf(m2, 1.0f - bb);
+  q = self ? -1.0f : fminf(m1, m2);
 }
-RT_FN void consider(Closest& C, float t, float q, float tmin, int ord, int pi) {
-  const float tc = (q >= 0.0f && t > tmin) ? t : __builtin_nanf("");
+// kKeyOnly (flat sets): only the key is tracked; t and the primitive follow from it afterwards
+template <bool kKeyOnly>
+RT_FN void consider(Closest& C, float t, float q, int ord, int pi) {
+  const float tc = q >= 0.0f ? t : __builtin_nanf("");
   const unsigned long long key = hit_key(tc, ord);
   const bool take = key < C.key;
   C.key = take ? key : C.key;
-  C.t = take ? tc : C.t;
-  C.prim = take ? pi : C.prim;
+  if constexpr (!kKeyOnly) {
+    C.t = take ? tc : C.t;
+    C.prim = take ? pi : C.prim;
+  }
 }
 
 // Any primitive record against the open interval (tmin, C.t).  When the record is wave-uniform
 // (flat sets) it sits in SGPRs and the kind / motion tests are scalar branches.
-RT_FN void test_rec(const KernelParams& P, const PrimRec& r, int pi, const RayCtx& R, float tmin, Closest& C) {
+template <bool kKeyOnly = false>
+RT_FN void test_rec(const KernelParams& P, const PrimRec& r, int pi, const RayCtx& R, float tmin, float tmin_up,
+                    Closest& C) {
   RT_COUNT(1);
   const int kf = RT_F2I(r.a.w);
   f3 o = R.o;
@@ -246,28 +263,28 @@ RT_FN void test_rec(const KernelParams& P, const PrimRec& r, int pi, const RayCt
   const bool self = RT_F2I(r.b.w) == R.self_gid;
   float t, q;
   if ((kf & RT_KIND_MASK) == 0)
-    isect_sphere(r, o, R, tmin, self, t, q);
+    isect_sphere(r, o, R, tmin, tmin_up, self, t, q);
   else if ((kf & RT_KIND_MASK) == 1)
-    isect_plane<true>(r, o, R, self, t, q);
+    isect_plane<true>(r, o, R, tmin_up, self, t, q);
   else
-    isect_plane<false>(r, o, R, self, t, q);
-  consider(C, t, q, tmin, RT_F2I(r.c.w), pi);
+    isect_plane<false>(r, o, R, tmin_up, self, t, q);
+  consider<kKeyOnly>(C, t, q, RT_F2I(r.c.w), pi);
 }
 
 // A static primitive of a known kind (flat sets are grouped by class: rt_build.cpp).
 template <int kKind>
-RT_FN void test_static(const PrimRec& r, int pi, const RayCtx& R, float tmin, Closest& C) {
+RT_FN void test_static(const PrimRec& r, const RayCtx& R, float tmin, float tmin_up, Closest& C) {
   RT_COUNT(1);
   const bool self = RT_F2I(r.b.w) == R.self_gid;
   float t, q;
   if constexpr (kKind == RT_PRIM_CLASS_SPHERE)
-    isect_sphere(r, R.o, R, tmin, self, t, q);
+    isect_sphere(r, R.o, R, tmin, tmin_up, self, t, q);
   else
-    isect_plane<kKind == RT_PRIM_CLASS_QUAD>(r, R.o, R, self, t, q);
-  consider(C, t, q, tmin, RT_F2I(r.c.w), pi);
+    isect_plane<kKind == RT_PRIM_CLASS_QUAD>(r, R.o, R, tmin_up, self, t, q);
+  consider<true>(C, t, q, RT_F2I(r.c.w), 0);
 }
 RT_FN void test_prim(const KernelParams& P, cfp pr, int pi, const RayCtx& R, float tmin, Closest& C) {
-  test_rec(P, ld_rec(pr), pi, R, tmin, C);
+  test_rec(P, ld_rec(pr), pi, R, tmin, float_up(tmin), C);
 }
 
 RT_FN void trace_leaf(const KernelParams& P, cfp prims, int first, int count, const RayCtx& R, float tmin,
@@ -343,10 +360,17 @@ RT_FN void closest(const KernelParams& P, cfp prims, int root, int set, const Ra
     // set comes from the kernel arguments: the ranges are wave-uniform, every loop is scalar
     const DevFlatSet& S = P.flat_sets[set];
     int k = S.first;
-    for (; k < S.end_quad; ++k) test_static<RT_PRIM_CLASS_QUAD>(ld_rec(prims + 16 * k), k, R, tmin, C);
-    for (; k < S.end_tri; ++k) test_static<RT_PRIM_CLASS_TRI>(ld_rec(prims + 16 * k), k, R, tmin, C);
-    for (; k < S.end_sphere; ++k) test_static<RT_PRIM_CLASS_SPHERE>(ld_rec(prims + 16 * k), k, R, tmin, C);
-    for (; k < S.end; ++k) test_rec(P, ld_rec(prims + 16 * k), k, R, tmin, C);
+    const RT_CAS PrimRec64* rp = (const RT_CAS PrimRec64*)prims + k;  // one 64-B scalar load per record
+    const float tmin_up = float_up(tmin);
+    for (; k < S.end_quad; ++k, ++rp) test_static<RT_PRIM_CLASS_QUAD>(ld_rec64(rp), R, tmin, tmin_up, C);
+    for (; k < S.end_tri; ++k, ++rp) test_static<RT_PRIM_CLASS_TRI>(ld_rec64(rp), R, tmin, tmin_up, C);
+    for (; k < S.end_sphere; ++k, ++rp) test_static<RT_PRIM_CLASS_SPHERE>(ld_rec64(rp), R, tmin, tmin_up, C);
+    for (; k < S.end; ++k, ++rp) test_rec<true>(P, ld_rec64(rp), k, R, tmin, tmin_up, C);
+    const uint32_t hi = (uint32_t)(C.key >> 32);
+    if (hi < 0x7f800000u) {  // a finite t won
+      C.t = __builtin_bit_cast(float, hi);
+      C.prim = ldci(P.flat_prim, (int)(uint32_t)C.key);
+    }
   } else {
     (void)set;
     trace_set(P, root, R, tmin, C, stack, stride, overflow);

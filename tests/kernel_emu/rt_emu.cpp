@@ -78,6 +78,7 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
   P.texs = H.texs.data();
   P.motions = H.motions.data();
   P.uvframes = H.uvframes.data();
+  P.flat_prim = H.flat_prim.data();
   P.out = out;
   P.surface_root = H.surface_root;
   P.n_media = H.n_media;
