@@ -26,7 +26,9 @@
 #define RT_STACK_DEPTH 32
 #define RT_MAX_MEDIA 8
 #define RT_MAX_TARGETS 8
+#ifndef RT_LEAF_MAX
 #define RT_LEAF_MAX 8
+#endif
 #define RT_LEAF_SHIFT 6       // leaf encoding ~(first << 6 | count - 1), count <= 64
 #define RT_FLAT_MAX 32        // a set of at most this many leaves is one flat leaf (no traversal)
 #define RT_LDS_PRIMS_MAX 256  // flat scenes whose leaves fit (16 KB) are staged in LDS

@@ -69,14 +69,14 @@ struct AtomicCommit {
 // kFlat = false: BVH scenes, dynamic LDS = the lanes' traversal stacks [depth][lane].
 // kFlat = true: every primitive set is one flat leaf; no LDS: the records are read with
 // wave-uniform addresses (scalar loads into SGPRs, scalar-cache resident).
-// Register budget: occupancy floor per variant (waves per SIMD).  The flat variant fits 5 waves
-// without VGPR spills; measured 7% faster on the Cornell box than the compiler's default of 4.
-// The BVH variant stays at 4 (5 and 6 spill and measured no faster on the mesh scenes).
+// Register budget: occupancy floor per variant (waves per SIMD).  Flat variant: 5 (measured 7%
+// faster on the Cornell box than the compiler's default of 4; it now fits 6 unforced).  BVH
+// variant: 5 (96 VGPRs, no spills; 4-6% faster than 4 on the bunny, pawn and demo1 scenes).
 #ifndef RT_WAVES_FLAT
 #define RT_WAVES_FLAT 5
 #endif
 #ifndef RT_WAVES_BVH
-#define RT_WAVES_BVH 4
+#define RT_WAVES_BVH 5
 #endif
 template <bool kFlat>
 __global__ __launch_bounds__(RT_BLOCK) __attribute__((amdgpu_waves_per_eu(kFlat ? RT_WAVES_FLAT : RT_WAVES_BVH)))

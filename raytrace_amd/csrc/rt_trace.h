@@ -49,6 +49,7 @@ extern thread_local long long counters[4];
 #define RT_RCP(x) (1.0f / (x))
 #define RT_SQRT(x) sqrtf(x)
 #define RT_COUNT(i) (++rt_emu::counters[i])
+#define RT_ANY(x) (x)  // the emulator runs one lane per wave
 #define RT_CAS
 #else
 #define RT_FN __device__ __forceinline__
@@ -59,6 +60,7 @@ extern thread_local long long counters[4];
 #define RT_RCP(x) __builtin_amdgcn_rcpf(x)
 #define RT_SQRT(x) __builtin_amdgcn_sqrtf(x)  // v_sqrt_f32 (1 ulp), no IEEE fix-up sequence
 #define RT_COUNT(i) ((void)0)
+#define RT_ANY(x) __any(x)
 // Scene data is read through the constant address space: the kernel never writes it, so
 // wave-uniform reads (flat sets, kernel-argument indices) become scalar loads into SGPRs and
 // divergent reads stay vector loads.
@@ -283,29 +285,41 @@ RT_FN void test_static(const PrimRec& r, const RayCtx& R, float tmin, float tmin
     isect_plane<kKind == RT_PRIM_CLASS_QUAD>(r, R.o, R, tmin_up, self, t, q);
   consider<true>(C, t, q, RT_F2I(r.c.w), 0);
 }
-RT_FN void test_prim(const KernelParams& P, cfp pr, int pi, const RayCtx& R, float tmin, Closest& C) {
-  test_rec(P, ld_rec(pr), pi, R, tmin, float_up(tmin), C);
-}
 
-RT_FN void trace_leaf(const KernelParams& P, cfp prims, int first, int count, const RayCtx& R, float tmin,
-                      Closest& C) {
-  for (int k = 0; k < count; ++k) test_prim(P, prims + 16 * (size_t)(first + k), first + k, R, tmin, C);
-}
 
 // Closest hit within (tmin, C.t) over one BVH; ties go to the smaller depth-first `order`
 // (the reference's group / bvhNode tie-break).  stack[k * stride] is this lane's stack.
+//
+// "While-while" traversal with postponed leaves (Aila & Laine, HPG 2009): a lane descends
+// interior nodes and, on reaching a leaf, parks it and keeps descending; the wave leaves the
+// interior loop only once every traversing lane holds a leaf (wave vote), then all lanes test
+// their leaves together.  Interior and leaf work never interleave within a wave step, which
+// otherwise serialises the two code paths across the 64 lanes.
 RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmin, Closest& C, int* stack,
                      int stride, int* overflow) {
   if (root == RT_EMPTY_ROOT) return;
+  constexpr int kDone = RT_EMPTY_ROOT;  // sentinel: stack exhausted
   int sp = 0;
   int node = root;
-  for (;;) {
-    if (node >= 0) {
+  int leaf = 0;  // parked leaf (negative encoding) or 0
+  if (root < 0) {  // the whole set is one leaf
+    leaf = root;
+    node = kDone;
+  }
+  const float tmin_up = float_up(tmin);
+  auto pop = [&]() -> int {
+    if (sp == 0) return kDone;
+    --sp;
+    return stack[sp * stride];
+  };
+  while (node != kDone || leaf != 0) {
+    // ---- interior phase
+    while (node >= 0) {
       RT_COUNT(0);
       cfp nd = cf(P.nodes) + 16 * (size_t)node;
       v4 n0 = ldc4(nd), n1 = ldc4(nd + 4), n2 = ldc4(nd + 8);
       const RT_CAS i4* n3p = (const RT_CAS i4*)(nd + 12);
-      i4 n3 = i4{n3p->x, n3p->y, n3p->z, n3p->w};
+      const int cl = n3p->x, cr = n3p->y;
       float lx0 = fmaf(n0.x, R.idir.x, -R.oidir.x), lx1 = fmaf(n0.y, R.idir.x, -R.oidir.x);
       float ly0 = fmaf(n0.z, R.idir.y, -R.oidir.y), ly1 = fmaf(n0.w, R.idir.y, -R.oidir.y);
       float lz0 = fmaf(n2.x, R.idir.z, -R.oidir.z), lz1 = fmaf(n2.y, R.idir.z, -R.oidir.z);
@@ -316,13 +330,10 @@ RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmi
       float lfar = fminf(fminf(fmaxf(lx0, lx1), fmaxf(ly0, ly1)), fminf(fmaxf(lz0, lz1), C.t));
       float rnear = fmaxf(fmaxf(fminf(rx0, rx1), fminf(ry0, ry1)), fmaxf(fminf(rz0, rz1), tmin));
       float rfar = fminf(fminf(fmaxf(rx0, rx1), fmaxf(ry0, ry1)), fminf(fmaxf(rz0, rz1), C.t));
-      bool hl = lnear <= lfar, hr = rnear <= rfar;
+      const bool hl = lnear <= lfar, hr = rnear <= rfar;
       if (hl && hr) {
-        int nearc = n3.x, farc = n3.y;
-        if (rnear < lnear) {
-          nearc = n3.y;
-          farc = n3.x;
-        }
+        const bool rfirst = rnear < lnear;
+        const int nearc = rfirst ? cr : cl, farc = rfirst ? cl : cr;
         if (sp < P.stack_depth) {
           stack[sp * stride] = farc;
           ++sp;
@@ -330,23 +341,29 @@ RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmi
           *overflow = 1;
         }
         node = nearc;
-        continue;
+      } else if (hl || hr) {
+        node = hl ? cl : cr;
+      } else {
+        node = pop();
       }
-      if (hl) {
-        node = n3.x;
-        continue;
+      if (node < 0 && node != kDone && leaf == 0) {  // park the first leaf, keep descending
+        leaf = node;
+        node = pop();
       }
-      if (hr) {
-        node = n3.y;
-        continue;
-      }
-    } else {
-      int enc = ~node;
-      trace_leaf(P, cf(P.prims), enc >> RT_LEAF_SHIFT, (enc & ((1 << RT_LEAF_SHIFT) - 1)) + 1, R, tmin, C);
+      if (!RT_ANY(leaf == 0)) break;  // every traversing lane holds a leaf
     }
-    if (sp == 0) break;
-    --sp;
-    node = stack[sp * stride];
+    // ---- leaf phase
+    while (leaf < 0) {
+      const int enc = ~leaf;
+      const int first = enc >> RT_LEAF_SHIFT, count = (enc & ((1 << RT_LEAF_SHIFT) - 1)) + 1;
+      for (int k = 0; k < count; ++k)
+        test_rec(P, ld_rec(cf(P.prims) + 16 * (size_t)(first + k)), first + k, R, tmin, tmin_up, C);
+      leaf = 0;
+      if (node < 0 && node != kDone) {  // the node we stopped at is a leaf too: test it next
+        leaf = node;
+        node = pop();
+      }
+    }
   }
 }
 
