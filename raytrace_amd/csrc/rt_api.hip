@@ -2,6 +2,7 @@
 // HBM, kernel launch (rt_kernel.hip), error reporting.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
@@ -62,6 +63,7 @@ struct rt_device_scene {
   DevFlatSet flat_sets[1 + RT_MAX_MEDIA];
   int n_nodes = 0, n_prims = 0, max_depth = 0;
   int stack_depth = 1;       // LDS stack entries per lane
+  int lds_nodes = 0;         // top surface-BVH nodes staged in LDS per workgroup
   bool flat = false;         // all sets are flat leaves: the LDS-resident variant
   int resident_blocks = 0;   // render-kernel workgroups resident on the device at that stack depth
   double upload_ms = 0;
@@ -140,7 +142,14 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
   s->max_depth = H.max_depth;
   s->stack_depth = H.max_depth > 1 ? H.max_depth : 1;
   s->flat = H.flat && std::getenv("RT_AMD_NO_FLAT") == nullptr;
-  s->resident_blocks = rt_render_resident_blocks(device, s->stack_depth, s->flat, H.n_prims);
+  if (!s->flat) {
+    // stage as many top (breadth-first) surface nodes as fit beside the stacks in the per-
+    // workgroup budget; env RT_AMD_LDS_NODES caps it (0 disables, for experiments)
+    const int room = (RT_LDS_WG_BUDGET - s->stack_depth * RT_BLOCK * (int)sizeof(int)) / 64;
+    s->lds_nodes = std::max(0, std::min(H.surface_nodes, room));
+    if (const char* e = std::getenv("RT_AMD_LDS_NODES")) s->lds_nodes = std::min(s->lds_nodes, std::max(0, atoi(e)));
+  }
+  s->resident_blocks = rt_render_resident_blocks(device, s->stack_depth, s->flat, s->lds_nodes);
   if (s->resident_blocks <= 0) {
     rt_scene_destroy(s);
     return fail(RT_E_HIP, "occupancy query failed");
@@ -183,6 +192,7 @@ int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint
   for (int k = 0; k < s->n_media; ++k) P.media[k] = s->media[k];
   for (int k = 0; k <= RT_MAX_MEDIA; ++k) P.flat_sets[k] = s->flat_sets[k];
   P.stack_depth = s->stack_depth;
+  P.lds_nodes = s->lds_nodes;
   P.n_prims = s->n_prims;
   rt_host_plan_work(P, (long long)s->resident_blocks * RT_BLOCK);
   HIP_TRY(hipSetDevice(s->device));

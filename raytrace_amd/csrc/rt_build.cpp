@@ -167,6 +167,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     roots[s] = bo.root;
     S.max_depth = std::max(S.max_depth, bo.max_depth);
     set_begin[s + 1] = (int)order.size();
+    if (s == 0) S.surface_nodes = (int)(S.nodes.size() / 16);
   }
   if (S.max_depth > RT_STACK_DEPTH)
     return fail(err, RT_E_STACK, "BVH depth %d exceeds the traversal stack (%d)", S.max_depth, RT_STACK_DEPTH);

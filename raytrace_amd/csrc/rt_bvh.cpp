@@ -166,18 +166,18 @@ void rt_build_bvh(std::vector<BuildPrim> prims, int node_base, int prim_base, Bv
   int root = B.build(0, (int)prims.size(), 0);
   out.max_depth = B.max_depth;
   for (auto& q : prims) out.order.push_back(q.index);
-  // number internal nodes in DFS order
+  // number internal nodes breadth-first: the top levels are the first nodes of the set, which
+  // is what the kernel stages in LDS (KernelParams::lds_nodes)
   std::vector<int> dev_index(B.tmp.size(), -1);
   std::vector<int> internal;
-  std::vector<int> st = {root};
-  while (!st.empty()) {
-    int id = st.back();
-    st.pop_back();
+  std::vector<int> queue = {root};
+  for (size_t head = 0; head < queue.size(); ++head) {
+    int id = queue[head];
     if (B.tmp[id].left < 0) continue;
     dev_index[id] = node_base + (int)internal.size();
     internal.push_back(id);
-    st.push_back(B.tmp[id].right);
-    st.push_back(B.tmp[id].left);
+    queue.push_back(B.tmp[id].left);
+    queue.push_back(B.tmp[id].right);
   }
   auto enc = [&](int id) -> int {
     const Node& nd = B.tmp[id];

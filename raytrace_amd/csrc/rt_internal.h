@@ -31,7 +31,8 @@
 #endif
 #define RT_LEAF_SHIFT 6       // leaf encoding ~(first << 6 | count - 1), count <= 64
 #define RT_FLAT_MAX 32        // a set of at most this many leaves is one flat leaf (no traversal)
-#define RT_LDS_PRIMS_MAX 256  // flat scenes whose leaves fit (16 KB) are staged in LDS
+#define RT_LDS_PRIMS_MAX 256  // flat kernel: scenes of at most this many primitives
+#define RT_LDS_WG_BUDGET 30720  // BVH kernel LDS per workgroup (stack + staged nodes): 5 per CU
 #define RT_EMPTY_ROOT ((int)0x80000000)
 
 #define RT_KIND_MASK 3
@@ -117,6 +118,7 @@ struct KernelParams {
   int n_chunks;
   int n_items;
   int stack_depth;            // LDS stack entries per lane (>= the scene's BVH depth)
+  int lds_nodes;              // BVH nodes [0, lds_nodes) are read from the workgroup's LDS copy
   int n_prims;                // all leaves (every set), staged in LDS by the flat kernel
   int surface_root;
   int n_media;
@@ -144,6 +146,7 @@ struct HostScene {
   DevMedium media[RT_MAX_MEDIA];
   DevFlatSet flat_sets[1 + RT_MAX_MEDIA] = {};
   int n_nodes = 0, n_prims = 0, max_depth = 0;
+  int surface_nodes = 0;  // nodes of the surface BVH: [0, surface_nodes), breadth-first
   bool flat = false;  // every set is a single flat leaf (no BVH nodes)
 };
 
@@ -162,7 +165,7 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
 // rt_kernel.hip (device launchers)
 // resident workgroups of the render kernel for a given LDS stack depth (occupancy query)
 // flat: the variant for scenes whose sets are all single flat leaves (prims staged in LDS)
-int rt_render_resident_blocks(int device, int stack_depth, bool flat, int n_prims);
+int rt_render_resident_blocks(int device, int stack_depth, bool flat, int lds_nodes);
 int rt_launch_render(const KernelParams& p, int grid_blocks, bool flat, void* stream);
 // accum / nanflag -> out (mean over spp, NaN where flagged)
 int rt_launch_resolve(const KernelParams& p, void* stream);

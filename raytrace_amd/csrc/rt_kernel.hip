@@ -86,9 +86,17 @@ void rt_render_kernel(KernelParams P) {
   AtomicCommit commit{P.accum, P.nanflag};
   int overflow;
   if constexpr (kFlat) {
-    overflow = rtk::lane_loop<true>(P, grab, commit, nullptr, 0, P.prims);
+    overflow = rtk::lane_loop<true>(P, grab, commit, rtk::Trav{nullptr, 0, nullptr}, P.prims);
   } else {
-    overflow = rtk::lane_loop<false>(P, grab, commit, smem + threadIdx.x, RT_BLOCK, P.prims);
+    // LDS: [stack_depth][RT_BLOCK] stack words, then the top P.lds_nodes BVH nodes (64 B each)
+    rtk::v4* lds_nodes = reinterpret_cast<rtk::v4*>(smem + P.stack_depth * RT_BLOCK);
+    const float4* src = reinterpret_cast<const float4*>(P.nodes);
+    for (int i = threadIdx.x; i < 4 * P.lds_nodes; i += RT_BLOCK) {
+      const float4 q = src[i];
+      lds_nodes[i] = rtk::v4{q.x, q.y, q.z, q.w};
+    }
+    __syncthreads();
+    overflow = rtk::lane_loop<false>(P, grab, commit, rtk::Trav{smem + threadIdx.x, RT_BLOCK, lds_nodes}, P.prims);
   }
   if (overflow) atomicOr(P.status, 1);
 }
@@ -142,14 +150,13 @@ __global__ __launch_bounds__(256) void rt_encode8_kernel(const float* __restrict
   }
 }
 
-static size_t render_lds_bytes(int stack_depth, bool flat, int n_prims) {
-  (void)n_prims;
-  return flat ? 0 : (size_t)stack_depth * RT_BLOCK * sizeof(int);
+static size_t render_lds_bytes(int stack_depth, bool flat, int lds_nodes) {
+  return flat ? 0 : (size_t)stack_depth * RT_BLOCK * sizeof(int) + (size_t)lds_nodes * 64;
 }
 
-int rt_render_resident_blocks(int device, int stack_depth, bool flat, int n_prims) {
+int rt_render_resident_blocks(int device, int stack_depth, bool flat, int lds_nodes) {
   int per_cu = 0, cus = 0;
-  size_t lds = render_lds_bytes(stack_depth, flat, n_prims);
+  size_t lds = render_lds_bytes(stack_depth, flat, lds_nodes);
   hipError_t e = flat ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<true>, RT_BLOCK, lds)
                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<false>, RT_BLOCK, lds);
   if (e != hipSuccess) return -1;
@@ -162,7 +169,7 @@ int rt_launch_render(const KernelParams& p, int grid_blocks, bool flat, void* st
   if (p.n_items <= 0 || grid_blocks <= 0) return 0;
   long long need = ((long long)p.n_items + RT_BLOCK - 1) / RT_BLOCK;
   int grid = need < grid_blocks ? (int)need : grid_blocks;
-  size_t lds = render_lds_bytes(p.stack_depth, flat, p.n_prims);
+  size_t lds = render_lds_bytes(p.stack_depth, flat, p.lds_nodes);
   if (flat)
     hipLaunchKernelGGL(rt_render_kernel<true>, dim3(grid), dim3(RT_BLOCK), lds, (hipStream_t)stream, p);
   else

@@ -187,6 +187,13 @@ struct Closest {
   unsigned long long key;
   int prim;
 };
+// Per-lane traversal resources: the lane's stack (stack[k * stride]) and the workgroup's LDS copy
+// of the first P.lds_nodes BVH nodes (breadth-first numbering puts the top levels there).
+struct Trav {
+  int* stack;
+  int stride;
+  const v4* lds_nodes;
+};
 RT_FN Closest no_hit() { return Closest{kInf, 0x7f80000000000000ull, -1}; }
 RT_FN unsigned long long hit_key(float t, int ord) {
   return ((unsigned long long)(unsigned)RT_F2I(t) << 32) | (unsigned)ord;
@@ -295,8 +302,10 @@ RT_FN void test_static(const PrimRec& r, const RayCtx& R, float tmin, float tmin
 // interior loop only once every traversing lane holds a leaf (wave vote), then all lanes test
 // their leaves together.  Interior and leaf work never interleave within a wave step, which
 // otherwise serialises the two code paths across the 64 lanes.
-RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmin, Closest& C, int* stack,
-                     int stride, int* overflow) {
+RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmin, Closest& C, const Trav& W,
+                     int* overflow) {
+  int* const stack = W.stack;
+  const int stride = W.stride;
   if (root == RT_EMPTY_ROOT) return;
   constexpr int kDone = RT_EMPTY_ROOT;  // sentinel: stack exhausted
   int sp = 0;
@@ -316,10 +325,24 @@ RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmi
     // ---- interior phase
     while (node >= 0) {
       RT_COUNT(0);
-      cfp nd = cf(P.nodes) + 16 * (size_t)node;
-      v4 n0 = ldc4(nd), n1 = ldc4(nd + 4), n2 = ldc4(nd + 8);
-      const RT_CAS i4* n3p = (const RT_CAS i4*)(nd + 12);
-      const int cl = n3p->x, cr = n3p->y;
+      v4 n0, n1, n2;
+      int cl, cr;
+      if (node < P.lds_nodes) {  // top levels of the surface BVH, staged in LDS per workgroup
+        const v4* nd = W.lds_nodes + 4 * node;
+        n0 = nd[0];
+        n1 = nd[1];
+        n2 = nd[2];
+        cl = RT_F2I(nd[3].x);
+        cr = RT_F2I(nd[3].y);
+      } else {
+        cfp nd = cf(P.nodes) + 16 * (size_t)node;
+        n0 = ldc4(nd);
+        n1 = ldc4(nd + 4);
+        n2 = ldc4(nd + 8);
+        const RT_CAS i4* n3p = (const RT_CAS i4*)(nd + 12);
+        cl = n3p->x;
+        cr = n3p->y;
+      }
       float lx0 = fmaf(n0.x, R.idir.x, -R.oidir.x), lx1 = fmaf(n0.y, R.idir.x, -R.oidir.x);
       float ly0 = fmaf(n0.z, R.idir.y, -R.oidir.y), ly1 = fmaf(n0.w, R.idir.y, -R.oidir.y);
       float lz0 = fmaf(n2.x, R.idir.z, -R.oidir.z), lz1 = fmaf(n2.y, R.idir.z, -R.oidir.z);
@@ -372,7 +395,7 @@ RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmi
 // and the records are read with scalar loads (uniform addresses).
 template <bool kFlat>
 RT_FN void closest(const KernelParams& P, cfp prims, int root, int set, const RayCtx& R, float tmin, Closest& C,
-                   int* stack, int stride, int* overflow) {
+                   const Trav& W, int* overflow) {
   if constexpr (kFlat) {
     // set comes from the kernel arguments: the ranges are wave-uniform, every loop is scalar
     const DevFlatSet& S = P.flat_sets[set];
@@ -390,7 +413,7 @@ RT_FN void closest(const KernelParams& P, cfp prims, int root, int set, const Ra
     }
   } else {
     (void)set;
-    trace_set(P, root, R, tmin, C, stack, stride, overflow);
+    trace_set(P, root, R, tmin, C, W, overflow);
   }
 }
 
@@ -494,7 +517,7 @@ RT_FN long long to_fixed(float x, bool& bad) {
 // The persistent lane loop.  `grab(need)` is wave-collective: it returns a fresh item for
 // lanes with need == true.  `commit(tile_pixel, sx, sy, sz, bad)` adds a finished item's sums.
 template <bool kFlat, class Grab, class Commit>
-RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, int* stack, int stride, const float* prims_) {
+RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW, const float* prims_) {
   const cfp prims = cf(prims_);
   int overflow = 0;
   const int W = P.cam.width, tile_pixels = P.tile_rows * W;
@@ -557,7 +580,7 @@ RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, int* stac
     R.idir = mk3(safe_rcp(R.d.x), safe_rcp(R.d.y), safe_rcp(R.d.z));
     R.oidir = R.o * R.idir;
     Closest C = no_hit();
-    closest<kFlat>(P, prims, P.surface_root, 0, R, kTmin, C, stack, stride, &overflow);
+    closest<kFlat>(P, prims, P.surface_root, 0, R, kTmin, C, TW, &overflow);
     float tbest = C.t;
     const int best = C.prim;
     int hit_medium = -1;
@@ -565,14 +588,14 @@ RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, int* stac
       // constantMedium (Geometry.hs:306-328)
       const DevMedium& M = P.media[m];
       Closest C1 = no_hit();
-      closest<kFlat>(P, prims, M.root, m + 1, R, kTmin, C1, stack, stride, &overflow);
+      closest<kFlat>(P, prims, M.root, m + 1, R, kTmin, C1, TW, &overflow);
       if (C1.prim < 0) continue;
       const float t1 = C1.t;
       float lo, hi;
       if (prim_front(P, prims, C1.prim, R, t1)) {
         if (!(t1 < tbest)) continue;
         Closest C2 = no_hit();
-        closest<kFlat>(P, prims, M.root, m + 1, R, t1, C2, stack, stride, &overflow);
+        closest<kFlat>(P, prims, M.root, m + 1, R, t1, C2, TW, &overflow);
         if (C2.prim < 0) continue;
         lo = t1;
         hi = C2.t;

@@ -50,8 +50,8 @@ void* worker(void* arg) {
   Grab g{s};
   Commit c{s};
   const bool flat = s->P->stack_depth == 0;  // the emulator marks flat scenes with depth 0
-  if (flat ? rtk::lane_loop<true>(*s->P, g, c, nullptr, 0, s->P->prims)
-           : rtk::lane_loop<false>(*s->P, g, c, stack.data(), 1, s->P->prims))
+  const rtk::Trav W{stack.data(), 1, nullptr};  // the emulator reads every node from memory
+  if (flat ? rtk::lane_loop<true>(*s->P, g, c, W, s->P->prims) : rtk::lane_loop<false>(*s->P, g, c, W, s->P->prims))
     s->overflow = 1;
   for (int i = 0; i < 4; ++i) s->cnt[i] += rt_emu::counters[i];
   return nullptr;
