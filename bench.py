@@ -50,10 +50,18 @@ def cpu_baseline(config, world_fn, row_stride=6):
     oracle.render(cs, world, seed, mode=oracle.RNG_SPLITMIX, pixels=pix, nthreads=threads)
     dt = time.perf_counter() - t0
     samples = len(pix) * cs.cs_samplesPerPixel
-    return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+    # single-core figure on a tenth of that sample (BASELINE.md §3 asks for both)
+    pix1 = pix.reshape(len(rows), w)[::10].reshape(-1)
+    t0 = time.perf_counter()
+    oracle.render(cs, world, seed, mode=oracle.RNG_SPLITMIX, pixels=pix1, nthreads=1)
+    dt1 = time.perf_counter() - t0
+    samples1 = len(pix1) * cs.cs_samplesPerPixel
+    return {"value": round(samples / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "value_1core": round(samples1 / dt1 / 1e6, 4), "host_cpus": os.cpu_count(),
             "sample": f"{config}: every {row_stride}th row ({len(rows)} rows x {w} px x {cs.cs_samplesPerPixel} spp"
                       f" = {samples / 1e6:.1f} M samples) in {dt:.2f} s, oracle/rt_oracle.c splitmix mode, "
-                      f"{threads} threads"}
+                      f"{threads} threads; 1-core: every {10 * row_stride}th row ({samples1 / 1e6:.2f} M samples)"
+                      f" in {dt1:.2f} s"}
 
 
 def pmc_traffic(config):

@@ -56,6 +56,9 @@ struct AtomicCommit {
   unsigned long long* accum;
   unsigned int* nanflag;
   __device__ __forceinline__ void operator()(int tp, long long sx, long long sy, long long sz, bool bad) const {
+#ifdef RT_EXP_NO_COMMIT  // ablation: drop the sums (wrong image), measures the cost of the atomics
+    if (sx != 12345) return;
+#endif
     unsigned long long* a = accum + 3 * (size_t)tp;
     if (sx) atomicAdd(a, (unsigned long long)sx);
     if (sy) atomicAdd(a + 1, (unsigned long long)sy);

@@ -399,13 +399,21 @@ RT_FN void closest(const KernelParams& P, cfp prims, int root, int set, const Ra
   if constexpr (kFlat) {
     // set comes from the kernel arguments: the ranges are wave-uniform, every loop is scalar
     const DevFlatSet& S = P.flat_sets[set];
+#ifdef RT_EXP_DOUBLE_TEST  // ablation: every flat set is tested twice (marginal cost of the tests)
+    for (int rep = 0; rep < 2; ++rep) {
+    const float tmin_up = float_up(tmin) + (float)rep * P.cam.pad;
+#else
+    const float tmin_up = float_up(tmin);
+#endif
     int k = S.first;
     const RT_CAS PrimRec64* rp = (const RT_CAS PrimRec64*)prims + k;  // one 64-B scalar load per record
-    const float tmin_up = float_up(tmin);
     for (; k < S.end_quad; ++k, ++rp) test_static<RT_PRIM_CLASS_QUAD>(ld_rec64(rp), R, tmin, tmin_up, C);
     for (; k < S.end_tri; ++k, ++rp) test_static<RT_PRIM_CLASS_TRI>(ld_rec64(rp), R, tmin, tmin_up, C);
     for (; k < S.end_sphere; ++k, ++rp) test_static<RT_PRIM_CLASS_SPHERE>(ld_rec64(rp), R, tmin, tmin_up, C);
     for (; k < S.end; ++k, ++rp) test_rec<true>(P, ld_rec64(rp), k, R, tmin, tmin_up, C);
+#ifdef RT_EXP_DOUBLE_TEST
+    }
+#endif
     const uint32_t hi = (uint32_t)(C.key >> 32);
     if (hi < 0x7f800000u) {  // a finite t won
       C.t = __builtin_bit_cast(float, hi);

@@ -24,12 +24,12 @@ for s in $STEPS; do
       done ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-        python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err" || { echo "rocprof failed"; tail -20 "$OUT/prof.err"; exit 1; }
+        python3 bench.py --steps ${PROF_STEPS:-20} --warmup 2 --no-cpu-baseline ${CONFIG:+--config $CONFIG} > "$OUT/prof_bench.json" 2> "$OUT/prof.err" || { echo "rocprof failed"; tail -20 "$OUT/prof.err"; exit 1; }
       find "$OUT/prof" -name "*kernel_stats.csv" -exec cat {} \; ;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$OUT/pmc_$c" -o run -- \
-          python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err" || { echo "pmc $c failed"; tail -20 "$OUT/pmc_$c.err"; exit 1; }
+          python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ${CONFIG:+--config $CONFIG} > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err" || { echo "pmc $c failed"; tail -20 "$OUT/pmc_$c.err"; exit 1; }
       done
       echo pmc done ;;
   esac
