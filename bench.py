@@ -12,9 +12,11 @@ tensor) inside the timed step; `value` = pixels x spp of all ranks / max-over-ra
 
 Extra fields: `roofline` (the render kernel's SURVEY.md §8(d) algorithmic bytes per launch /
 its HIP-event-timed duration vs the 8 TB/s HBM peak; `traffic` = PMC-measured HBM bytes per
-launch from the committed rocprofv3 summary, when present) and `cpu_baseline` (the FP64
-oracle, the CPU restatement of the reference's algorithm, on a bounded row sample, rank 0 at
-N=1 only).
+launch from the committed rocprofv3 summary, when present), `issue_roofline` (the kernel's
+PMC-counted VALU wave-instructions per launch / its time vs the chip's VALU issue ceiling — the
+physical limiter of this cache-resident, branchy FP32 kernel) and `cpu_baseline`
+(the FP64 oracle, the CPU restatement of the reference's algorithm, on a bounded row sample,
+rank 0 at N=1 only, with a 1-core figure beside the threaded one).
 """
 import argparse
 import json
@@ -75,6 +77,25 @@ def pmc_traffic(config):
         return d.get(config, {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
+
+
+# VALU issue ceiling: 256 CUs x 4 SIMD-32 x one wave64 VALU instruction per 2 cycles at the
+# 2.4 GHz peak engine clock (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles")
+VALU_PEAK_GINST = 256 * 4 * 0.5 * 2.4
+
+
+def pmc_valu(config, kernel_ms):
+    """Issue roofline of the render kernel from the committed PMC VALU counts (profiles/pmc_valu.json)."""
+    path = os.path.join(ROOT, "profiles", "pmc_valu.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)[config]
+    except Exception:
+        return None
+    ach = d["valu_insts_per_launch"] / (kernel_ms * 1e-3) / 1e9
+    return {"bound": "valu-issue", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
+            "frac": round(ach / VALU_PEAK_GINST, 4), "lane_utilisation": round(d["lane_utilisation"], 4),
+            "valu_insts_per_launch": d["valu_insts_per_launch"], "pmc_round": d.get("round")}
 
 
 def main():
@@ -190,7 +211,8 @@ def main():
                        "width": w, "height": h, "spp": spp, "max_depth": cs.cs_maxRecursionDepth,
                        "parallelism": f"rows interleaved over {n} GPU(s), row_block {args.row_block}"
                                       + (", RCCL all_gather of the framebuffer" if n > 1 else "")},
-            "roofline": roofline, "cpu_baseline": cpu, "check": check,
+            "roofline": roofline, "issue_roofline": pmc_valu(args.config, kernel_ms), "cpu_baseline": cpu,
+            "check": check,
         }
         print(json.dumps(line), flush=True)
     if n > 1:
