@@ -64,7 +64,7 @@ struct rt_device_scene {
   int n_nodes = 0, n_prims = 0, max_depth = 0;
   int stack_depth = 1;       // LDS stack entries per lane
   int lds_nodes = 0;         // top surface-BVH nodes staged in LDS per workgroup
-  bool flat = false;         // all sets are flat leaves: the LDS-resident variant
+  int variant = RT_VAR_FLAT;  // render-kernel variant (rt_internal.h RT_VAR_*)
   int resident_blocks = 0;   // render-kernel workgroups resident on the device at that stack depth
   double upload_ms = 0;
 };
@@ -141,15 +141,15 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
   s->n_prims = H.n_prims;
   s->max_depth = H.max_depth;
   s->stack_depth = H.max_depth > 1 ? H.max_depth : 1;
-  s->flat = H.flat && std::getenv("RT_AMD_NO_FLAT") == nullptr;
-  if (!s->flat) {
+  s->variant = rt_host_variant(H.flat, H.n_media);
+  if (s->variant != RT_VAR_FLAT) {
     // stage as many top (breadth-first) surface nodes as fit beside the stacks in the per-
     // workgroup budget; env RT_AMD_LDS_NODES caps it (0 disables, for experiments)
     const int room = (RT_LDS_WG_BUDGET - s->stack_depth * RT_BLOCK * (int)sizeof(int)) / 64;
     s->lds_nodes = std::max(0, std::min(H.surface_nodes, room));
     if (const char* e = std::getenv("RT_AMD_LDS_NODES")) s->lds_nodes = std::min(s->lds_nodes, std::max(0, atoi(e)));
   }
-  s->resident_blocks = rt_render_resident_blocks(device, s->stack_depth, s->flat, s->lds_nodes);
+  s->resident_blocks = rt_render_resident_blocks(device, s->stack_depth, s->variant, s->lds_nodes);
   if (s->resident_blocks <= 0) {
     rt_scene_destroy(s);
     return fail(RT_E_HIP, "occupancy query failed");
@@ -209,7 +209,7 @@ int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint
   P.nanflag = (unsigned int*)(ws + off_flag);
   P.counter = (int*)(ws + off_ctr);
   rc = RT_OK;
-  if (rt_launch_render(P, s->resident_blocks, s->flat, hip_stream) || rt_launch_resolve(P, hip_stream))
+  if (rt_launch_render(P, s->resident_blocks, s->variant, hip_stream) || rt_launch_resolve(P, hip_stream))
     rc = fail(RT_E_HIP, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
   HIP_TRY(hipFreeAsync(ws, st));
   return rc;

@@ -284,6 +284,16 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   return RT_OK;
 }
 
+int rt_host_variant(bool flat, int n_media) {
+  int v = flat ? RT_VAR_FLAT : (n_media > 0 ? RT_VAR_BVH_LOCKSTEP : RT_VAR_BVH);
+  if (const char* e = std::getenv("RT_AMD_VARIANT")) {
+    const int f = atoi(e);
+    if (!flat && (f == RT_VAR_BVH_LOCKSTEP || f == RT_VAR_BVH)) v = f;  // flat scenes run on any variant
+    if (flat && f >= RT_VAR_FLAT && f <= RT_VAR_BVH) v = f;
+  }
+  return v;
+}
+
 int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex, KernelParams& P,
                         std::string& err) {
   if (!cs || !ex) return fail(err, RT_E_INVALID, "null argument");
@@ -362,6 +372,8 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
 }
 
 void rt_host_plan_work(KernelParams& P, long long resident_lanes) {
+  P.trav_exit_pct = 50;
+  if (const char* e = std::getenv("RT_AMD_TRAV_PCT")) P.trav_exit_pct = std::max(0, std::min(100, atoi(e)));
   // Items = (tile pixel, chunk of consecutive samples), claimed in pixel order.  Small chunks
   // keep the 64 lanes of a wave on neighbouring pixels (coherent rays) and make the queue tail
   // short; below ~2 samples the per-item commit (3 atomics) dominates.  Measured on MI355X,

@@ -35,6 +35,13 @@
 #define RT_LDS_WG_BUDGET 30720  // BVH kernel LDS per workgroup (stack + staged nodes): 5 per CU
 #define RT_EMPTY_ROOT ((int)0x80000000)
 
+// render-kernel variants (rt_kernel.hip)
+#define RT_VAR_FLAT 0          // every set one flat leaf, lockstep lane loop
+#define RT_VAR_BVH_LOCKSTEP 1  // BVH, lockstep lane loop (scenes with media)
+#define RT_VAR_BVH 2           // BVH, traversal decoupled from shading (no media)
+// host choice of variant (rt_build.cpp); env RT_AMD_VARIANT overrides for experiments
+int rt_host_variant(bool flat, int n_media);
+
 #define RT_KIND_MASK 3
 #define RT_FLAG_MOTION 4
 
@@ -119,6 +126,7 @@ struct KernelParams {
   int n_items;
   int stack_depth;            // LDS stack entries per lane (>= the scene's BVH depth)
   int lds_nodes;              // BVH nodes [0, lds_nodes) are read from the workgroup's LDS copy
+  int trav_exit_pct;          // BVH kernel: leave traversal when <= this % of live lanes trace
   int n_prims;                // all leaves (every set), staged in LDS by the flat kernel
   int surface_root;
   int n_media;
@@ -165,8 +173,8 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
 // rt_kernel.hip (device launchers)
 // resident workgroups of the render kernel for a given LDS stack depth (occupancy query)
 // flat: the variant for scenes whose sets are all single flat leaves (prims staged in LDS)
-int rt_render_resident_blocks(int device, int stack_depth, bool flat, int lds_nodes);
-int rt_launch_render(const KernelParams& p, int grid_blocks, bool flat, void* stream);
+int rt_render_resident_blocks(int device, int stack_depth, int variant, int lds_nodes);
+int rt_launch_render(const KernelParams& p, int grid_blocks, int variant, void* stream);
 // accum / nanflag -> out (mean over spp, NaN where flagged)
 int rt_launch_resolve(const KernelParams& p, void* stream);
 // work decomposition (rt_build.cpp): chunk so that items >= ~8 x resident lanes

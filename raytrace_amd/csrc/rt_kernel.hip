@@ -69,27 +69,32 @@ struct AtomicCommit {
 
 }  // namespace
 
-// kFlat = false: BVH scenes, dynamic LDS = the lanes' traversal stacks [depth][lane].
-// kFlat = true: every primitive set is one flat leaf; no LDS: the records are read with
-// wave-uniform addresses (scalar loads into SGPRs, scalar-cache resident).
-// Register budget: occupancy floor per variant (waves per SIMD).  Flat variant: 5 (measured 7%
-// faster on the Cornell box than the compiler's default of 4; it now fits 6 unforced).  BVH
-// variant: 5 (96 VGPRs, no spills; 4-6% faster than 4 on the bunny, pawn and demo1 scenes).
+// Variants (rt_internal.h RT_VAR_*), chosen per scene by the host:
+//  RT_VAR_FLAT: every primitive set is one flat leaf; no LDS: the records are read with
+//    wave-uniform addresses (scalar loads into SGPRs, scalar-cache resident); lockstep loop.
+//  RT_VAR_BVH_LOCKSTEP / RT_VAR_BVH: BVH scenes; dynamic LDS = the lanes' traversal stacks
+//    [depth][lane] followed by the top P.lds_nodes nodes.  Scenes without media use the
+//    decoupled loop (traversal and shading interleaved per lane, rt_trace.h lane_loop_bvh);
+//    scenes with media the lockstep loop, whose per-segment query chain stays coherent.
+// Register budget: occupancy floor (waves per SIMD).  Flat: 5 (measured 7% faster on the Cornell
+// box than the compiler's default of 4; it now fits 6 unforced).  BVH: 5 (96 VGPRs; faster
+// than 4 on the bunny, pawn and demo1 scenes).
 #ifndef RT_WAVES_FLAT
 #define RT_WAVES_FLAT 5
 #endif
 #ifndef RT_WAVES_BVH
 #define RT_WAVES_BVH 5
 #endif
-template <bool kFlat>
-__global__ __launch_bounds__(RT_BLOCK) __attribute__((amdgpu_waves_per_eu(kFlat ? RT_WAVES_FLAT : RT_WAVES_BVH)))
+template <int kVar>
+__global__ __launch_bounds__(RT_BLOCK)
+__attribute__((amdgpu_waves_per_eu(kVar == RT_VAR_FLAT ? RT_WAVES_FLAT : RT_WAVES_BVH)))
 void rt_render_kernel(KernelParams P) {
   extern __shared__ int smem[];
   WaveGrab grab{P.counter, 0, 0};
   AtomicCommit commit{P.accum, P.nanflag};
   int overflow;
-  if constexpr (kFlat) {
-    overflow = rtk::lane_loop<true>(P, grab, commit, rtk::Trav{nullptr, 0, nullptr}, P.prims);
+  if constexpr (kVar == RT_VAR_FLAT) {
+    overflow = rtk::lane_loop_lockstep<true>(P, grab, commit, rtk::Trav{nullptr, 0, nullptr}, P.prims);
   } else {
     // LDS: [stack_depth][RT_BLOCK] stack words, then the top P.lds_nodes BVH nodes (64 B each)
     rtk::v4* lds_nodes = reinterpret_cast<rtk::v4*>(smem + P.stack_depth * RT_BLOCK);
@@ -99,7 +104,11 @@ void rt_render_kernel(KernelParams P) {
       lds_nodes[i] = rtk::v4{q.x, q.y, q.z, q.w};
     }
     __syncthreads();
-    overflow = rtk::lane_loop<false>(P, grab, commit, rtk::Trav{smem + threadIdx.x, RT_BLOCK, lds_nodes}, P.prims);
+    const rtk::Trav W{smem + threadIdx.x, RT_BLOCK, lds_nodes};
+    if constexpr (kVar == RT_VAR_BVH_LOCKSTEP)
+      overflow = rtk::lane_loop_lockstep<false>(P, grab, commit, W, P.prims);
+    else
+      overflow = rtk::lane_loop_bvh(P, grab, commit, W, P.prims);
   }
   if (overflow) atomicOr(P.status, 1);
 }
@@ -153,30 +162,39 @@ __global__ __launch_bounds__(256) void rt_encode8_kernel(const float* __restrict
   }
 }
 
-static size_t render_lds_bytes(int stack_depth, bool flat, int lds_nodes) {
-  return flat ? 0 : (size_t)stack_depth * RT_BLOCK * sizeof(int) + (size_t)lds_nodes * 64;
+static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
+  return variant == RT_VAR_FLAT ? 0 : (size_t)stack_depth * RT_BLOCK * sizeof(int) + (size_t)lds_nodes * 64;
 }
 
-int rt_render_resident_blocks(int device, int stack_depth, bool flat, int lds_nodes) {
+template <int kVar>
+static hipError_t occupancy(int* per_cu, size_t lds) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, rt_render_kernel<kVar>, RT_BLOCK, lds);
+}
+
+int rt_render_resident_blocks(int device, int stack_depth, int variant, int lds_nodes) {
   int per_cu = 0, cus = 0;
-  size_t lds = render_lds_bytes(stack_depth, flat, lds_nodes);
-  hipError_t e = flat ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<true>, RT_BLOCK, lds)
-                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_render_kernel<false>, RT_BLOCK, lds);
+  size_t lds = render_lds_bytes(stack_depth, variant, lds_nodes);
+  hipError_t e = variant == RT_VAR_FLAT            ? occupancy<RT_VAR_FLAT>(&per_cu, lds)
+                 : variant == RT_VAR_BVH_LOCKSTEP ? occupancy<RT_VAR_BVH_LOCKSTEP>(&per_cu, lds)
+                                                   : occupancy<RT_VAR_BVH>(&per_cu, lds);
   if (e != hipSuccess) return -1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return -1;
   if (per_cu < 1) per_cu = 1;
   return per_cu * cus;
 }
 
-int rt_launch_render(const KernelParams& p, int grid_blocks, bool flat, void* stream) {
+int rt_launch_render(const KernelParams& p, int grid_blocks, int variant, void* stream) {
   if (p.n_items <= 0 || grid_blocks <= 0) return 0;
   long long need = ((long long)p.n_items + RT_BLOCK - 1) / RT_BLOCK;
   int grid = need < grid_blocks ? (int)need : grid_blocks;
-  size_t lds = render_lds_bytes(p.stack_depth, flat, p.lds_nodes);
-  if (flat)
-    hipLaunchKernelGGL(rt_render_kernel<true>, dim3(grid), dim3(RT_BLOCK), lds, (hipStream_t)stream, p);
+  size_t lds = render_lds_bytes(p.stack_depth, variant, p.lds_nodes);
+  hipStream_t st = (hipStream_t)stream;
+  if (variant == RT_VAR_FLAT)
+    hipLaunchKernelGGL(rt_render_kernel<RT_VAR_FLAT>, dim3(grid), dim3(RT_BLOCK), lds, st, p);
+  else if (variant == RT_VAR_BVH_LOCKSTEP)
+    hipLaunchKernelGGL(rt_render_kernel<RT_VAR_BVH_LOCKSTEP>, dim3(grid), dim3(RT_BLOCK), lds, st, p);
   else
-    hipLaunchKernelGGL(rt_render_kernel<false>, dim3(grid), dim3(RT_BLOCK), lds, (hipStream_t)stream, p);
+    hipLaunchKernelGGL(rt_render_kernel<RT_VAR_BVH>, dim3(grid), dim3(RT_BLOCK), lds, st, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -33,6 +33,7 @@
 #include <cmath>
 #include <cstring>
 #define RT_FN static inline
+#define RT_FN_SPEC inline  // explicit specialisations take no storage class
 namespace rt_emu {
 inline int f2i(float f) {
   int i;
@@ -50,9 +51,11 @@ extern thread_local long long counters[4];
 #define RT_SQRT(x) sqrtf(x)
 #define RT_COUNT(i) (++rt_emu::counters[i])
 #define RT_ANY(x) (x)  // the emulator runs one lane per wave
+#define RT_BALLOT_COUNT(x) ((x) ? 1 : 0)
 #define RT_CAS
 #else
 #define RT_FN __device__ __forceinline__
+#define RT_FN_SPEC __device__ __forceinline__
 #define RT_F2I(f) __float_as_int(f)
 #define RT_SINCOS(x, s, c) __sincosf(x, s, c)
 #define RT_LOG(x) __logf(x)
@@ -61,6 +64,7 @@ extern thread_local long long counters[4];
 #define RT_SQRT(x) __builtin_amdgcn_sqrtf(x)  // v_sqrt_f32 (1 ulp), no IEEE fix-up sequence
 #define RT_COUNT(i) ((void)0)
 #define RT_ANY(x) __any(x)
+#define RT_BALLOT_COUNT(x) ((int)__popcll(__ballot(x)))
 // Scene data is read through the constant address space: the kernel never writes it, so
 // wave-uniform reads (flat sets, kernel-argument indices) become scalar loads into SGPRs and
 // divergent reads stay vector loads.
@@ -294,136 +298,12 @@ RT_FN void test_static(const PrimRec& r, const RayCtx& R, float tmin, float tmin
 }
 
 
-// Closest hit within (tmin, C.t) over one BVH; ties go to the smaller depth-first `order`
-// (the reference's group / bvhNode tie-break).  stack[k * stride] is this lane's stack.
-//
-// "While-while" traversal with postponed leaves (Aila & Laine, HPG 2009): a lane descends
-// interior nodes and, on reaching a leaf, parks it and keeps descending; the wave leaves the
-// interior loop only once every traversing lane holds a leaf (wave vote), then all lanes test
-// their leaves together.  Interior and leaf work never interleave within a wave step, which
-// otherwise serialises the two code paths across the 64 lanes.
-RT_FN void trace_set(const KernelParams& P, int root, const RayCtx& R, float tmin, Closest& C, const Trav& W,
-                     int* overflow) {
-  int* const stack = W.stack;
-  const int stride = W.stride;
-  if (root == RT_EMPTY_ROOT) return;
-  constexpr int kDone = RT_EMPTY_ROOT;  // sentinel: stack exhausted
-  int sp = 0;
-  int node = root;
-  int leaf = 0;  // parked leaf (negative encoding) or 0
-  if (root < 0) {  // the whole set is one leaf
-    leaf = root;
-    node = kDone;
-  }
-  const float tmin_up = float_up(tmin);
-  auto pop = [&]() -> int {
-    if (sp == 0) return kDone;
-    --sp;
-    return stack[sp * stride];
-  };
-  while (node != kDone || leaf != 0) {
-    // ---- interior phase
-    while (node >= 0) {
-      RT_COUNT(0);
-      v4 n0, n1, n2;
-      int cl, cr;
-      if (node < P.lds_nodes) {  // top levels of the surface BVH, staged in LDS per workgroup
-        const v4* nd = W.lds_nodes + 4 * node;
-        n0 = nd[0];
-        n1 = nd[1];
-        n2 = nd[2];
-        cl = RT_F2I(nd[3].x);
-        cr = RT_F2I(nd[3].y);
-      } else {
-        cfp nd = cf(P.nodes) + 16 * (size_t)node;
-        n0 = ldc4(nd);
-        n1 = ldc4(nd + 4);
-        n2 = ldc4(nd + 8);
-        const RT_CAS i4* n3p = (const RT_CAS i4*)(nd + 12);
-        cl = n3p->x;
-        cr = n3p->y;
-      }
-      float lx0 = fmaf(n0.x, R.idir.x, -R.oidir.x), lx1 = fmaf(n0.y, R.idir.x, -R.oidir.x);
-      float ly0 = fmaf(n0.z, R.idir.y, -R.oidir.y), ly1 = fmaf(n0.w, R.idir.y, -R.oidir.y);
-      float lz0 = fmaf(n2.x, R.idir.z, -R.oidir.z), lz1 = fmaf(n2.y, R.idir.z, -R.oidir.z);
-      float rx0 = fmaf(n1.x, R.idir.x, -R.oidir.x), rx1 = fmaf(n1.y, R.idir.x, -R.oidir.x);
-      float ry0 = fmaf(n1.z, R.idir.y, -R.oidir.y), ry1 = fmaf(n1.w, R.idir.y, -R.oidir.y);
-      float rz0 = fmaf(n2.z, R.idir.z, -R.oidir.z), rz1 = fmaf(n2.w, R.idir.z, -R.oidir.z);
-      float lnear = fmaxf(fmaxf(fminf(lx0, lx1), fminf(ly0, ly1)), fmaxf(fminf(lz0, lz1), tmin));
-      float lfar = fminf(fminf(fmaxf(lx0, lx1), fmaxf(ly0, ly1)), fminf(fmaxf(lz0, lz1), C.t));
-      float rnear = fmaxf(fmaxf(fminf(rx0, rx1), fminf(ry0, ry1)), fmaxf(fminf(rz0, rz1), tmin));
-      float rfar = fminf(fminf(fmaxf(rx0, rx1), fmaxf(ry0, ry1)), fminf(fmaxf(rz0, rz1), C.t));
-      const bool hl = lnear <= lfar, hr = rnear <= rfar;
-      if (hl && hr) {
-        const bool rfirst = rnear < lnear;
-        const int nearc = rfirst ? cr : cl, farc = rfirst ? cl : cr;
-        if (sp < P.stack_depth) {
-          stack[sp * stride] = farc;
-          ++sp;
-        } else {
-          *overflow = 1;
-        }
-        node = nearc;
-      } else if (hl || hr) {
-        node = hl ? cl : cr;
-      } else {
-        node = pop();
-      }
-      if (node < 0 && node != kDone && leaf == 0) {  // park the first leaf, keep descending
-        leaf = node;
-        node = pop();
-      }
-      if (!RT_ANY(leaf == 0)) break;  // every traversing lane holds a leaf
-    }
-    // ---- leaf phase
-    while (leaf < 0) {
-      const int enc = ~leaf;
-      const int first = enc >> RT_LEAF_SHIFT, count = (enc & ((1 << RT_LEAF_SHIFT) - 1)) + 1;
-      for (int k = 0; k < count; ++k)
-        test_rec(P, ld_rec(cf(P.prims) + 16 * (size_t)(first + k)), first + k, R, tmin, tmin_up, C);
-      leaf = 0;
-      if (node < 0 && node != kDone) {  // the node we stopped at is a leaf too: test it next
-        leaf = node;
-        node = pop();
-      }
-    }
-  }
-}
-
 // Closest hit over one primitive set.  kFlat: the set is a single flat leaf (RT_FLAT_MAX
 // leaves at most): every lane walks the same records in the same order, so the loop is coherent
 // and the records are read with scalar loads (uniform addresses).
 template <bool kFlat>
 RT_FN void closest(const KernelParams& P, cfp prims, int root, int set, const RayCtx& R, float tmin, Closest& C,
-                   const Trav& W, int* overflow) {
-  if constexpr (kFlat) {
-    // set comes from the kernel arguments: the ranges are wave-uniform, every loop is scalar
-    const DevFlatSet& S = P.flat_sets[set];
-#ifdef RT_EXP_DOUBLE_TEST  // ablation: every flat set is tested twice (marginal cost of the tests)
-    for (int rep = 0; rep < 2; ++rep) {
-    const float tmin_up = float_up(tmin) + (float)rep * P.cam.pad;
-#else
-    const float tmin_up = float_up(tmin);
-#endif
-    int k = S.first;
-    const RT_CAS PrimRec64* rp = (const RT_CAS PrimRec64*)prims + k;  // one 64-B scalar load per record
-    for (; k < S.end_quad; ++k, ++rp) test_static<RT_PRIM_CLASS_QUAD>(ld_rec64(rp), R, tmin, tmin_up, C);
-    for (; k < S.end_tri; ++k, ++rp) test_static<RT_PRIM_CLASS_TRI>(ld_rec64(rp), R, tmin, tmin_up, C);
-    for (; k < S.end_sphere; ++k, ++rp) test_static<RT_PRIM_CLASS_SPHERE>(ld_rec64(rp), R, tmin, tmin_up, C);
-    for (; k < S.end; ++k, ++rp) test_rec<true>(P, ld_rec64(rp), k, R, tmin, tmin_up, C);
-#ifdef RT_EXP_DOUBLE_TEST
-    }
-#endif
-    const uint32_t hi = (uint32_t)(C.key >> 32);
-    if (hi < 0x7f800000u) {  // a finite t won
-      C.t = __builtin_bit_cast(float, hi);
-      C.prim = ldci(P.flat_prim, (int)(uint32_t)C.key);
-    }
-  } else {
-    (void)set;
-    trace_set(P, root, R, tmin, C, W, overflow);
-  }
-}
+                   const Trav& W, int* overflow);
 
 struct HitInfo {
   f3 p, n;
@@ -522,17 +402,362 @@ RT_FN long long to_fixed(float x, bool& bad) {
 #endif
 }
 
-// The persistent lane loop.  `grab(need)` is wave-collective: it returns a fresh item for
-// lanes with need == true.  `commit(tile_pixel, sx, sy, sz, bad)` adds a finished item's sums.
+// ---------------------------------------------------------------- BVH traversal
+// Resumable per-lane BVH traversal (the body of trace_set, split so a lane can stop between
+// rounds and continue in a later iteration of the lane loop with its state intact).
+struct TravState {
+  int node, leaf, sp;
+  float tmin, tmin_up;
+  Closest C;
+};
+RT_FN void trav_begin(TravState& S, int root, float tmin) {
+  S.node = root;
+  S.leaf = 0;
+  S.sp = 0;
+  if (root < 0) {  // an empty set, or a set that is one leaf
+    S.leaf = root == RT_EMPTY_ROOT ? 0 : root;
+    S.node = RT_EMPTY_ROOT;
+  }
+  S.tmin = tmin;
+  S.tmin_up = float_up(tmin);
+  S.C = no_hit();
+}
+RT_FN bool trav_done(const TravState& S) { return S.node == RT_EMPTY_ROOT && S.leaf == 0; }
+
+// One while-while round: descend until this lane (and the wave) holds a leaf, then test leaves.
+RT_FN void trav_round(const KernelParams& P, const RayCtx& R, TravState& S, const Trav& W, int& overflow) {
+  constexpr int kDone = RT_EMPTY_ROOT;
+  int* const stack = W.stack;
+  const int stride = W.stride;
+  auto pop = [&]() -> int {
+    if (S.sp == 0) return kDone;
+    --S.sp;
+    return stack[S.sp * stride];
+  };
+  while (S.node >= 0) {
+    RT_COUNT(0);
+    v4 n0, n1, n2;
+    int cl, cr;
+    const int node = S.node;
+    if (node < P.lds_nodes) {  // top levels of the surface BVH, staged in LDS per workgroup
+      const v4* nd = W.lds_nodes + 4 * node;
+      n0 = nd[0];
+      n1 = nd[1];
+      n2 = nd[2];
+      cl = RT_F2I(nd[3].x);
+      cr = RT_F2I(nd[3].y);
+    } else {
+      cfp nd = cf(P.nodes) + 16 * (size_t)node;
+      n0 = ldc4(nd);
+      n1 = ldc4(nd + 4);
+      n2 = ldc4(nd + 8);
+      const RT_CAS i4* n3p = (const RT_CAS i4*)(nd + 12);
+      cl = n3p->x;
+      cr = n3p->y;
+    }
+    float lx0 = fmaf(n0.x, R.idir.x, -R.oidir.x), lx1 = fmaf(n0.y, R.idir.x, -R.oidir.x);
+    float ly0 = fmaf(n0.z, R.idir.y, -R.oidir.y), ly1 = fmaf(n0.w, R.idir.y, -R.oidir.y);
+    float lz0 = fmaf(n2.x, R.idir.z, -R.oidir.z), lz1 = fmaf(n2.y, R.idir.z, -R.oidir.z);
+    float rx0 = fmaf(n1.x, R.idir.x, -R.oidir.x), rx1 = fmaf(n1.y, R.idir.x, -R.oidir.x);
+    float ry0 = fmaf(n1.z, R.idir.y, -R.oidir.y), ry1 = fmaf(n1.w, R.idir.y, -R.oidir.y);
+    float rz0 = fmaf(n2.z, R.idir.z, -R.oidir.z), rz1 = fmaf(n2.w, R.idir.z, -R.oidir.z);
+    float lnear = fmaxf(fmaxf(fminf(lx0, lx1), fminf(ly0, ly1)), fmaxf(fminf(lz0, lz1), S.tmin));
+    float lfar = fminf(fminf(fmaxf(lx0, lx1), fmaxf(ly0, ly1)), fminf(fmaxf(lz0, lz1), S.C.t));
+    float rnear = fmaxf(fmaxf(fminf(rx0, rx1), fminf(ry0, ry1)), fmaxf(fminf(rz0, rz1), S.tmin));
+    float rfar = fminf(fminf(fmaxf(rx0, rx1), fmaxf(ry0, ry1)), fminf(fmaxf(rz0, rz1), S.C.t));
+    const bool hl = lnear <= lfar, hr = rnear <= rfar;
+    if (hl && hr) {
+      const bool rfirst = rnear < lnear;
+      const int nearc = rfirst ? cr : cl, farc = rfirst ? cl : cr;
+      if (S.sp < P.stack_depth) {
+        stack[S.sp * stride] = farc;
+        ++S.sp;
+      } else {
+        overflow = 1;
+      }
+      S.node = nearc;
+    } else if (hl || hr) {
+      S.node = hl ? cl : cr;
+    } else {
+      S.node = pop();
+    }
+    if (S.node < 0 && S.node != kDone && S.leaf == 0) {  // park the first leaf, keep descending
+      S.leaf = S.node;
+      S.node = pop();
+    }
+    if (!RT_ANY(S.leaf == 0)) break;  // every traversing lane holds a leaf
+  }
+  while (S.leaf < 0) {
+    const int enc = ~S.leaf;
+    const int first = enc >> RT_LEAF_SHIFT, count = (enc & ((1 << RT_LEAF_SHIFT) - 1)) + 1;
+    for (int k = 0; k < count; ++k)
+      test_rec(P, ld_rec(cf(P.prims) + 16 * (size_t)(first + k)), first + k, R, S.tmin, S.tmin_up, S.C);
+    S.leaf = 0;
+    if (S.node < 0 && S.node != kDone) {  // the node we stopped at is a leaf too: test it next
+      S.leaf = S.node;
+      S.node = pop();
+    }
+  }
+}
+
+// kFlat: the set is one flat leaf (rt_internal.h DevFlatSet); every lane walks the same
+// records in the same order, so the loops are coherent and the records are scalar loads.
+template <>
+RT_FN_SPEC void closest<true>(const KernelParams& P, cfp prims, int root, int set, const RayCtx& R, float tmin, Closest& C,
+                         const Trav& W, int* overflow) {
+  (void)root;
+  (void)W;
+  (void)overflow;
+  {
+    // set comes from the kernel arguments: the ranges are wave-uniform, every loop is scalar
+    const DevFlatSet& S = P.flat_sets[set];
+#ifdef RT_EXP_DOUBLE_TEST  // ablation: every flat set is tested twice (marginal cost of the tests)
+    for (int rep = 0; rep < 2; ++rep) {
+    const float tmin_up = float_up(tmin) + (float)rep * P.cam.pad;
+#else
+    const float tmin_up = float_up(tmin);
+#endif
+    int k = S.first;
+    const RT_CAS PrimRec64* rp = (const RT_CAS PrimRec64*)prims + k;  // one 64-B scalar load per record
+    for (; k < S.end_quad; ++k, ++rp) test_static<RT_PRIM_CLASS_QUAD>(ld_rec64(rp), R, tmin, tmin_up, C);
+    for (; k < S.end_tri; ++k, ++rp) test_static<RT_PRIM_CLASS_TRI>(ld_rec64(rp), R, tmin, tmin_up, C);
+    for (; k < S.end_sphere; ++k, ++rp) test_static<RT_PRIM_CLASS_SPHERE>(ld_rec64(rp), R, tmin, tmin_up, C);
+    for (; k < S.end; ++k, ++rp) test_rec<true>(P, ld_rec64(rp), k, R, tmin, tmin_up, C);
+#ifdef RT_EXP_DOUBLE_TEST
+    }
+#endif
+    const uint32_t hi = (uint32_t)(C.key >> 32);
+    if (hi < 0x7f800000u) {  // a finite t won
+      C.t = __builtin_bit_cast(float, hi);
+      C.prim = ldci(P.flat_prim, (int)(uint32_t)C.key);
+    }
+  }
+}
+
+// BVH set (lockstep variant): resumable rounds run to completion.
+template <>
+RT_FN_SPEC void closest<false>(const KernelParams& P, cfp prims, int root, int set, const RayCtx& R, float tmin,
+                          Closest& C, const Trav& W, int* overflow) {
+  (void)prims;
+  (void)set;
+  TravState S;
+  trav_begin(S, root, tmin);
+  while (!trav_done(S)) trav_round(P, R, S, W, *overflow);
+  C = S.C;
+}
+
+// ------------------------------------------------------------------ per-path pieces
+// Ray.hs:157-172, 229: pixel jitter, time, defocus-disk point -> primary ray
+RT_FN void camera_ray(const KernelParams& P, uint32_t pix, int sample, int px, int gy, RayCtx& R) {
+  u4 w0 = philox(pix, (uint32_t)sample, 0u, RT_EV_CAMERA0, P.key0, P.key1);
+  R.time = u01(w0.z);
+  f3 origin = ld3(P.cam.center);
+  if (P.cam.disk_u[0] != 0.0f || P.cam.disk_u[1] != 0.0f || P.cam.disk_u[2] != 0.0f || P.cam.disk_v[0] != 0.0f ||
+      P.cam.disk_v[1] != 0.0f || P.cam.disk_v[2] != 0.0f) {
+    u4 w1 = philox(pix, (uint32_t)sample, 0u, RT_EV_CAMERA1, P.key0, P.key1);
+    float rad = sqrtf(u01(w0.w)), s, c;
+    RT_SINCOS(2.0f * kPi * u01(w1.x), &s, &c);
+    origin = origin + (rad * c) * ld3(P.cam.disk_u) + (rad * s) * ld3(P.cam.disk_v);
+  }
+  f3 target = ld3(P.cam.top_left) + ((float)px + u01(w0.x)) * ld3(P.cam.pixel_u) +
+              ((float)gy + u01(w0.y)) * ld3(P.cam.pixel_v);
+  R.o = origin;
+  R.d = normalize(target - origin);
+  R.self_gid = -1;
+}
+
+RT_FN void prep_ray(RayCtx& R) {
+  R.idir = mk3(safe_rcp(R.d.x), safe_rcp(R.d.y), safe_rcp(R.d.z));
+  R.oidir = R.o * R.idir;
+}
+
+// constantMedium's free-flight draw over the segment (lo, hi) (Geometry.hs:312-328); wm is the
+// Philox block of event RT_EV_MEDIA + m / 4 of this segment
+RT_FN void medium_draw(const KernelParams& P, int m, u4 wm, float lo, float hi, float& tbest, int& hit_medium) {
+  uint32_t wsel = (m & 3) == 0 ? wm.x : (m & 3) == 1 ? wm.y : (m & 3) == 2 ? wm.z : wm.w;
+  float rnd = 1.0f - u01(wsel);
+  float hit_dist = P.media[m].neg_inv_density * RT_LOG(rnd);
+  if (hit_dist < hi - lo) {
+    float t = lo + hit_dist;
+    if (t < tbest) {
+      tbest = t;
+      hit_medium = m;
+    }
+  }
+}
+RT_FN u4 medium_block(const KernelParams& P, int m, uint32_t pix, int sample, int seg) {
+  return philox(pix, (uint32_t)sample, (uint32_t)seg, RT_EV_MEDIA + (uint32_t)(m >> 2), P.key0, P.key1);
+}
+RT_FN void medium_event(const KernelParams& P, int m, uint32_t pix, int sample, int seg, float lo, float hi,
+                        float& tbest, int& hit_medium) {
+  medium_draw(P, m, medium_block(P, m, pix, sample, seg), lo, hi, tbest, hit_medium);
+}
+
+// One rayColor level after the closest hit (Ray.hs:176-224): background on a miss, else the
+// material of the surface / medium hit.  Updates L, T and, when the path continues, the ray
+// (and seg).  Returns true when the path terminates.
+RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int& seg, float tbest, int best,
+                 int hit_medium, RayCtx& R, f3& L, f3& T) {
+  RT_HOOK_SEGMENT(pix, sample, seg, R, tbest, best, hit_medium, L, T);
+  if (hit_medium < 0 && best < 0) {
+    // miss: cs_background (Ray.hs:179)
+    f3 bg = ld3(P.cam.bg0);
+    if (P.cam.bg_kind == 1) {
+      float a = 0.5f * (R.d.y + 1.0f);
+      bg = (1.0f - a) * bg + a * ld3(P.cam.bg1);
+    }
+    L = L + T * bg;
+    return true;
+  }
+  bool terminate = false;
+  HitInfo h;
+  if (hit_medium >= 0) {
+    h.p = R.o + tbest * R.d;
+    h.n = -R.d;
+    h.front = true;
+    h.u = 0.f;
+    h.v = 0.f;
+    h.mat = P.media[hit_medium].material;
+    h.gid = -1;
+  } else {
+    h = surface_info(P, prims, best, R, tbest);
+  }
+  const RT_CAS DevMaterial* Mp = (const RT_CAS DevMaterial*)P.mats + h.mat;
+  const DevMaterial Mt = DevMaterial{Mp->kind, Mp->tex, Mp->param, 0};
+  u4 w = philox(pix, (uint32_t)sample, (uint32_t)seg, RT_EV_SCATTER, P.key0, P.key1);
+  const bool last = seg + 1 >= P.cam.max_depth;  // rayColor (depth - 1) with depth - 1 <= 0 is zero
+  f3 newdir = R.d;
+  switch (Mt.kind) {
+    case 0:  // lightSource: emit, Absorb
+      L = L + T * eval_texture(P, Mt.tex, h.u, h.v);
+      terminate = true;
+      break;
+    case 1:  // pitchBlack
+      terminate = true;
+      break;
+    case 4:  // mirror
+      T = T * eval_texture(P, Mt.tex, h.u, h.v);
+      newdir = unit(reflect(h.n, R.d));
+      break;
+    case 5: {  // metal
+      f3 d2 = reflect(h.n, R.d) + Mt.param * unit_vector(w.y, w.z);
+      if (dot(d2, h.n) > 0.0f) {
+        T = T * eval_texture(P, Mt.tex, h.u, h.v);
+        newdir = normalize(d2);
+      } else {
+        terminate = true;
+      }
+      break;
+    }
+    case 6: {  // dielectric
+      float ior = Mt.param;
+      float ratio = h.front ? RT_RCP(ior) : ior;
+      float cos_t = fminf(1.0f, -dot(h.n, R.d));
+      float sin_t = sqrtf(fmaxf(0.0f, 1.0f - cos_t * cos_t));
+      float r0 = (1.0f - ratio) * RT_RCP(1.0f + ratio);
+      r0 = r0 * r0;
+      float x1 = 1.0f - cos_t, x2 = x1 * x1;
+      float reflectance = r0 + (1.0f - r0) * (x2 * x2 * x1);
+      if (ratio * sin_t > 1.0f || u01(w.x) < reflectance) {
+        newdir = unit(reflect(h.n, R.d));
+      } else {
+        f3 perp = ratio * (R.d + cos_t * h.n);
+        newdir = unit(perp - sqrtf(fabsf(1.0f - dot(perp, perp))) * h.n);
+      }
+      break;
+    }
+    case 7:  // transparent
+      T = T * eval_texture(P, Mt.tex, h.u, h.v);
+      break;
+    default: {  // 2 lambertian, 3 lommelSeeliger (HemisphereF); 8 isotropic, 9 anisotropic (SphereF)
+      const bool hemi = Mt.kind == 2 || Mt.kind == 3;
+      float cr = u01(w.x);
+      int choice = -1;
+      for (int k = 0; k < P.n_targets; ++k) {
+        if (cr < P.targets[k].thresh) {
+          choice = k;
+          break;
+        }
+      }
+      f3 dir;
+      if (choice < 0) {
+        f3 uu = unit_vector(w.y, w.z);
+        dir = hemi ? normalize(h.n + uu) : uu;
+      } else {
+        const DevTarget& Tg = P.targets[choice];
+        f3 lp = ld3(Tg.q) + u01(w.y) * ld3(Tg.u) + u01(w.z) * ld3(Tg.v);
+        dir = normalize(lp - h.p);
+      }
+      float pdf1 = hemi ? dot(dir, h.n) * (1.0f / kPi) : 0.25f / kPi;
+      if (hemi && pdf1 <= 0.0f) {
+        terminate = true;
+        break;
+      }
+      float mix = 0.0f;
+      for (int k = 0; k < P.n_targets; ++k) {
+        float tt;
+        if (target_hit(P.targets[k], h.p, dir, tt))
+          mix += P.targets[k].prob * (tt * tt * RT_RCP(fabsf(dot(ld3(P.targets[k].cr), dir))));
+      }
+      float pdf = P.rem_prob * pdf1 + mix;
+      f3 f = eval_texture(P, Mt.tex, h.u, h.v);
+      if (Mt.kind == 3) {
+        float mu0 = -dot(R.d, h.n), mu1 = dot(dir, h.n);
+        f = (0.25f * RT_RCP(mu0 + mu1)) * f;
+      } else if (Mt.kind == 9) {
+        float g = Mt.param, mu = dot(R.d, dir);
+        float base = 1.0f + g * g - 2.0f * g * mu;
+        f = ((1.0f - g * g) * RT_RCP(base * sqrtf(base))) * f;
+      }
+      T = T * ((pdf1 * RT_RCP(pdf)) * f);
+      newdir = dir;
+      break;
+    }
+  }
+  if (!terminate) {
+    if (last) {
+      terminate = true;
+    } else {
+      R.o = h.p;
+      R.d = newdir;
+      R.self_gid = h.gid;
+      ++seg;
+    }
+  }
+  return terminate;
+}
+
+// Work item -> pixel / sample range (items are claimed in pixel order, chunk index slowest).
+struct ItemCtx {
+  int item, tp, px, gy, sample, s_end;
+  uint32_t pix;
+};
+RT_FN bool open_item(const KernelParams& P, int item, ItemCtx& I) {
+  const int W = P.cam.width, tile_pixels = P.tile_rows * W;
+  I.item = item;
+  const int k = item / tile_pixels;
+  I.tp = item - k * tile_pixels;
+  const int tr = I.tp / W;
+  I.px = I.tp - tr * W;
+  I.gy = ((tr / P.row_block) * P.n_shards + P.shard) * P.row_block + (tr % P.row_block);
+  I.pix = (uint32_t)(I.gy * W + I.px);
+  I.sample = k * P.chunk;
+  I.s_end = I.sample + P.chunk < P.cam.spp ? I.sample + P.chunk : P.cam.spp;
+  if (I.gy >= P.cam.height || P.cam.max_depth <= 0) I.s_end = I.sample;  // padding row / black image
+  return I.sample < I.s_end;
+}
+
+// The lockstep persistent lane loop.  `grab(need)` is wave-collective: it returns a fresh item
+// for lanes with need == true.  `commit(tile_pixel, sx, sy, sz, bad)` adds a finished item's
+// sums.  One segment per iteration, all of its queries run by the whole wave together: the flat
+// kernel (every lane tests the same primitives) and the BVH kernel of scenes with media.
 template <bool kFlat, class Grab, class Commit>
-RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW, const float* prims_) {
+RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW,
+                             const float* prims_) {
   const cfp prims = cf(prims_);
   int overflow = 0;
-  const int W = P.cam.width, tile_pixels = P.tile_rows * W;
-  const int spp = P.cam.spp, max_depth = P.cam.max_depth;
-  int item = -1, tp = 0, sample = 0, s_end = 0, seg = 0;
-  int px = 0, gy = 0;
-  uint32_t pix = 0;
+  ItemCtx I{-1, 0, 0, 0, 0, 0, 0u};
+  int seg = 0;
   long long sx = 0, sy = 0, sz = 0;
   bool bad = false;
   bool alive = false;
@@ -542,42 +767,17 @@ RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, const Tra
   R.time = 0.0f;
   R.self_gid = -1;
   for (;;) {
-    const bool need = !alive && sample >= s_end;
-    if (need && item >= 0) commit(tp, sx, sy, sz, bad);
+    const bool need = !alive && I.sample >= I.s_end;
+    if (need && I.item >= 0) commit(I.tp, sx, sy, sz, bad);
     const int got = grab(need);
     if (need) {
-      item = got;
-      if (item >= P.n_items) break;
-      const int k = item / tile_pixels;
-      tp = item - k * tile_pixels;
-      const int tr = tp / W;
-      px = tp - tr * W;
-      gy = ((tr / P.row_block) * P.n_shards + P.shard) * P.row_block + (tr % P.row_block);
-      pix = (uint32_t)(gy * W + px);
-      sample = k * P.chunk;
-      s_end = sample + P.chunk < spp ? sample + P.chunk : spp;
-      if (gy >= P.cam.height || max_depth <= 0) s_end = sample;  // padding row / black image
+      if (got >= P.n_items) break;
       sx = sy = sz = 0;
       bad = false;
-      if (sample >= s_end) continue;
+      if (!open_item(P, got, I)) continue;
     }
     if (!alive) {
-      // Ray.hs:157-172, 229: pixel jitter, time, defocus-disk point
-      u4 w0 = philox(pix, (uint32_t)sample, 0u, RT_EV_CAMERA0, P.key0, P.key1);
-      R.time = u01(w0.z);
-      f3 origin = ld3(P.cam.center);
-      if (P.cam.disk_u[0] != 0.0f || P.cam.disk_u[1] != 0.0f || P.cam.disk_u[2] != 0.0f ||
-          P.cam.disk_v[0] != 0.0f || P.cam.disk_v[1] != 0.0f || P.cam.disk_v[2] != 0.0f) {
-        u4 w1 = philox(pix, (uint32_t)sample, 0u, RT_EV_CAMERA1, P.key0, P.key1);
-        float rad = sqrtf(u01(w0.w)), s, c;
-        RT_SINCOS(2.0f * kPi * u01(w1.x), &s, &c);
-        origin = origin + (rad * c) * ld3(P.cam.disk_u) + (rad * s) * ld3(P.cam.disk_v);
-      }
-      f3 target = ld3(P.cam.top_left) + ((float)px + u01(w0.x)) * ld3(P.cam.pixel_u) +
-                  ((float)gy + u01(w0.y)) * ld3(P.cam.pixel_v);
-      R.o = origin;
-      R.d = normalize(target - origin);
-      R.self_gid = -1;
+      camera_ray(P, I.pix, I.sample, I.px, I.gy, R);
       L = mk3(0.f, 0.f, 0.f);
       T = mk3(1.f, 1.f, 1.f);
       seg = 0;
@@ -585,8 +785,7 @@ RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, const Tra
     }
     RT_COUNT(2);
     // ---- closest hit over the surfaces and every medium (Ray.hs:178)
-    R.idir = mk3(safe_rcp(R.d.x), safe_rcp(R.d.y), safe_rcp(R.d.z));
-    R.oidir = R.o * R.idir;
+    prep_ray(R);
     Closest C = no_hit();
     closest<kFlat>(P, prims, P.surface_root, 0, R, kTmin, C, TW, &overflow);
     float tbest = C.t;
@@ -611,152 +810,136 @@ RT_FN int lane_loop(const KernelParams& P, Grab& grab, Commit& commit, const Tra
         lo = kTmin;
         hi = t1;
       }
-      u4 wm = philox(pix, (uint32_t)sample, (uint32_t)seg, RT_EV_MEDIA + (uint32_t)(m >> 2), P.key0, P.key1);
-      uint32_t wsel = (m & 3) == 0 ? wm.x : (m & 3) == 1 ? wm.y : (m & 3) == 2 ? wm.z : wm.w;
-      float rnd = 1.0f - u01(wsel);
-      float hit_dist = M.neg_inv_density * RT_LOG(rnd);
-      if (hit_dist < hi - lo) {
-        float t = lo + hit_dist;
-        if (t < tbest) {
-          tbest = t;
-          hit_medium = m;
-        }
-      }
+      medium_event(P, m, I.pix, I.sample, seg, lo, hi, tbest, hit_medium);
     }
-    RT_HOOK_SEGMENT(pix, sample, seg, R, tbest, best, hit_medium, L, T);
-    bool terminate = false;
-    if (hit_medium < 0 && best < 0) {
-      // miss: cs_background (Ray.hs:179)
-      f3 bg = ld3(P.cam.bg0);
-      if (P.cam.bg_kind == 1) {
-        float a = 0.5f * (R.d.y + 1.0f);
-        bg = (1.0f - a) * bg + a * ld3(P.cam.bg1);
-      }
-      L = L + T * bg;
-      terminate = true;
-    } else {
-      HitInfo h;
-      if (hit_medium >= 0) {
-        h.p = R.o + tbest * R.d;
-        h.n = -R.d;
-        h.front = true;
-        h.u = 0.f;
-        h.v = 0.f;
-        h.mat = P.media[hit_medium].material;
-        h.gid = -1;
-      } else {
-        h = surface_info(P, prims, best, R, tbest);
-      }
-      const RT_CAS DevMaterial* Mp = (const RT_CAS DevMaterial*)P.mats + h.mat;
-      const DevMaterial Mt = DevMaterial{Mp->kind, Mp->tex, Mp->param, 0};
-      u4 w = philox(pix, (uint32_t)sample, (uint32_t)seg, RT_EV_SCATTER, P.key0, P.key1);
-      const bool last = seg + 1 >= max_depth;  // rayColor (depth - 1) with depth - 1 <= 0 is zero
-      f3 newdir = R.d;
-      switch (Mt.kind) {
-        case 0:  // lightSource: emit, Absorb
-          L = L + T * eval_texture(P, Mt.tex, h.u, h.v);
-          terminate = true;
-          break;
-        case 1:  // pitchBlack
-          terminate = true;
-          break;
-        case 4:  // mirror
-          T = T * eval_texture(P, Mt.tex, h.u, h.v);
-          newdir = unit(reflect(h.n, R.d));
-          break;
-        case 5: {  // metal
-          f3 d2 = reflect(h.n, R.d) + Mt.param * unit_vector(w.y, w.z);
-          if (dot(d2, h.n) > 0.0f) {
-            T = T * eval_texture(P, Mt.tex, h.u, h.v);
-            newdir = normalize(d2);
-          } else {
-            terminate = true;
-          }
-          break;
-        }
-        case 6: {  // dielectric
-          float ior = Mt.param;
-          float ratio = h.front ? RT_RCP(ior) : ior;
-          float cos_t = fminf(1.0f, -dot(h.n, R.d));
-          float sin_t = sqrtf(fmaxf(0.0f, 1.0f - cos_t * cos_t));
-          float r0 = (1.0f - ratio) * RT_RCP(1.0f + ratio);
-          r0 = r0 * r0;
-          float x1 = 1.0f - cos_t, x2 = x1 * x1;
-          float reflectance = r0 + (1.0f - r0) * (x2 * x2 * x1);
-          if (ratio * sin_t > 1.0f || u01(w.x) < reflectance) {
-            newdir = unit(reflect(h.n, R.d));
-          } else {
-            f3 perp = ratio * (R.d + cos_t * h.n);
-            newdir = unit(perp - sqrtf(fabsf(1.0f - dot(perp, perp))) * h.n);
-          }
-          break;
-        }
-        case 7:  // transparent
-          T = T * eval_texture(P, Mt.tex, h.u, h.v);
-          break;
-        default: {  // 2 lambertian, 3 lommelSeeliger (HemisphereF); 8 isotropic, 9 anisotropic (SphereF)
-          const bool hemi = Mt.kind == 2 || Mt.kind == 3;
-          float cr = u01(w.x);
-          int choice = -1;
-          for (int k = 0; k < P.n_targets; ++k) {
-            if (cr < P.targets[k].thresh) {
-              choice = k;
-              break;
-            }
-          }
-          f3 dir;
-          if (choice < 0) {
-            f3 uu = unit_vector(w.y, w.z);
-            dir = hemi ? normalize(h.n + uu) : uu;
-          } else {
-            const DevTarget& Tg = P.targets[choice];
-            f3 lp = ld3(Tg.q) + u01(w.y) * ld3(Tg.u) + u01(w.z) * ld3(Tg.v);
-            dir = normalize(lp - h.p);
-          }
-          float pdf1 = hemi ? dot(dir, h.n) * (1.0f / kPi) : 0.25f / kPi;
-          if (hemi && pdf1 <= 0.0f) {
-            terminate = true;
-            break;
-          }
-          float mix = 0.0f;
-          for (int k = 0; k < P.n_targets; ++k) {
-            float tt;
-            if (target_hit(P.targets[k], h.p, dir, tt))
-              mix += P.targets[k].prob * (tt * tt * RT_RCP(fabsf(dot(ld3(P.targets[k].cr), dir))));
-          }
-          float pdf = P.rem_prob * pdf1 + mix;
-          f3 f = eval_texture(P, Mt.tex, h.u, h.v);
-          if (Mt.kind == 3) {
-            float mu0 = -dot(R.d, h.n), mu1 = dot(dir, h.n);
-            f = (0.25f * RT_RCP(mu0 + mu1)) * f;
-          } else if (Mt.kind == 9) {
-            float g = Mt.param, mu = dot(R.d, dir);
-            float base = 1.0f + g * g - 2.0f * g * mu;
-            f = ((1.0f - g * g) * RT_RCP(base * sqrtf(base))) * f;
-          }
-          T = T * ((pdf1 * RT_RCP(pdf)) * f);
-          newdir = dir;
-          break;
-        }
-      }
-      if (!terminate) {
-        if (last) {
-          terminate = true;
-        } else {
-          R.o = h.p;
-          R.d = newdir;
-          R.self_gid = h.gid;
-          ++seg;
-        }
-      }
-    }
-    if (terminate) {
-      RT_HOOK_SAMPLE(pix, sample, L);
+    if (shade(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T)) {
+      RT_HOOK_SAMPLE(I.pix, I.sample, L);
       sx += to_fixed(L.x, bad);
       sy += to_fixed(L.y, bad);
       sz += to_fixed(L.z, bad);
       alive = false;
-      ++sample;
+      ++I.sample;
+    }
+  }
+  return overflow;
+}
+
+// The persistent lane loop of the BVH kernel, with traversal decoupled from shading inside the
+// wave.  Incoherent secondary rays need very different numbers of traversal rounds; if every
+// lane waited for the wave's slowest traversal before shading, most lanes would idle (measured
+// ~21 % lane utilisation).  Here a lane is in one of the states below; the wave runs traversal
+// rounds for the TRACE lanes until at most P.trav_exit_pct % of the loop's live lanes still
+// trace, then lets the others shade and start their next ray, and goes back to traversal with
+// the stragglers keeping their traversal state (stack in LDS).  A segment's queries run in the
+// reference's order — the surfaces, then per medium its first boundary hit and, for a ray
+// entering it, the second (Geometry.hs:306-328) — each starting inside the traversal loop as
+// soon as the previous one finishes.
+enum : int { ST_NEED_ITEM = 0, ST_NEED_SAMPLE = 1, ST_START_SEG = 2, ST_TRACE = 3, ST_SHADE = 4 };
+template <class Grab, class Commit>
+RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW, const float* prims_) {
+  const cfp prims = cf(prims_);
+  int overflow = 0;
+  ItemCtx I{-1, 0, 0, 0, 0, 0, 0u};
+  int seg = 0;
+  long long sx = 0, sy = 0, sz = 0;
+  bool bad = false;
+  int state = ST_NEED_ITEM;
+  f3 L = mk3(0.f, 0.f, 0.f), T = mk3(1.f, 1.f, 1.f);
+  RayCtx R;
+  R.o = R.d = R.idir = R.oidir = L;
+  R.time = 0.0f;
+  R.self_gid = -1;
+  TravState S;
+  trav_begin(S, RT_EMPTY_ROOT, kTmin);
+  // query sequencing within a segment: q = 0 surfaces; q = 1 + 2m / 2 + 2m medium m, 1st / 2nd hit
+  int q = 0, best = -1, hit_medium = -1;
+  float tbest = kInf, t1 = 0.0f;
+  for (;;) {
+    // ---- front end: items, samples, segment starts (lanes not tracing)
+    const bool need = state == ST_NEED_ITEM;
+    if (need && I.item >= 0) commit(I.tp, sx, sy, sz, bad);
+    const int got = grab(need);
+    if (need) {
+      if (got >= P.n_items) break;
+      sx = sy = sz = 0;
+      bad = false;
+      state = open_item(P, got, I) ? ST_NEED_SAMPLE : ST_NEED_ITEM;
+    }
+    if (state == ST_NEED_SAMPLE) {
+      camera_ray(P, I.pix, I.sample, I.px, I.gy, R);
+      L = mk3(0.f, 0.f, 0.f);
+      T = mk3(1.f, 1.f, 1.f);
+      seg = 0;
+      state = ST_START_SEG;
+    }
+    if (state == ST_START_SEG) {
+      RT_COUNT(2);
+      prep_ray(R);
+      q = 0;
+      best = -1;
+      hit_medium = -1;
+      tbest = kInf;
+      trav_begin(S, P.surface_root, kTmin);
+      state = ST_TRACE;
+    }
+    // ---- traversal rounds; a finished query starts the segment's next one in place
+    for (;;) {
+      const bool tr = state == ST_TRACE;
+      const int n_tr = RT_BALLOT_COUNT(tr);
+      if (n_tr == 0) break;
+      const int n_live = RT_BALLOT_COUNT(true);
+      if (n_tr < n_live && n_tr * 100 <= n_live * P.trav_exit_pct) break;
+      if (tr) {
+        trav_round(P, R, S, TW, overflow);
+        if (trav_done(S)) {
+          int next_m = -1;  // medium whose first query starts next
+          if (q == 0) {
+            tbest = S.C.t;
+            best = S.C.prim;
+            next_m = 0;
+          } else {
+            const int m = (q - 1) >> 1;
+            next_m = m + 1;
+            if ((q & 1) == 1) {  // first boundary hit of medium m
+              if (S.C.prim >= 0) {
+                t1 = S.C.t;
+                if (prim_front(P, prims, S.C.prim, R, t1)) {
+                  if (t1 < tbest) {  // entering: the exit hit bounds the segment
+                    q = q + 1;
+                    trav_begin(S, P.media[m].root, t1);
+                    next_m = -1;
+                  }
+                } else {
+                  medium_event(P, m, I.pix, I.sample, seg, kTmin, t1, tbest, hit_medium);
+                }
+              }
+            } else if (S.C.prim >= 0) {  // exit hit of medium m
+              medium_event(P, m, I.pix, I.sample, seg, t1, S.C.t, tbest, hit_medium);
+            }
+          }
+          if (next_m >= 0) {
+            if (next_m < P.n_media) {
+              q = 1 + 2 * next_m;
+              trav_begin(S, P.media[next_m].root, kTmin);
+            } else {
+              state = ST_SHADE;
+            }
+          }
+        }
+      }
+    }
+    // ---- shade the segments whose queries are complete
+    if (state == ST_SHADE) {
+      if (shade(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T)) {
+        RT_HOOK_SAMPLE(I.pix, I.sample, L);
+        sx += to_fixed(L.x, bad);
+        sy += to_fixed(L.y, bad);
+        sz += to_fixed(L.z, bad);
+        ++I.sample;
+        state = I.sample < I.s_end ? ST_NEED_SAMPLE : ST_NEED_ITEM;
+      } else {
+        state = ST_START_SEG;
+      }
     }
   }
   return overflow;

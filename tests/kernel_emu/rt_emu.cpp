@@ -22,6 +22,7 @@ thread_local std::string g_err;
 
 struct Shared {
   const KernelParams* P;
+  int variant;
   std::atomic<int> next{0};
   std::atomic<int> overflow{0};
   std::vector<std::atomic<long long>>* accum;
@@ -49,9 +50,15 @@ void* worker(void* arg) {
   for (auto& c : rt_emu::counters) c = 0;
   Grab g{s};
   Commit c{s};
-  const bool flat = s->P->stack_depth == 0;  // the emulator marks flat scenes with depth 0
   const rtk::Trav W{stack.data(), 1, nullptr};  // the emulator reads every node from memory
-  if (flat ? rtk::lane_loop<true>(*s->P, g, c, W, s->P->prims) : rtk::lane_loop<false>(*s->P, g, c, W, s->P->prims))
+  int ov = 0;
+  if (s->variant == RT_VAR_FLAT)
+    ov = rtk::lane_loop_lockstep<true>(*s->P, g, c, W, s->P->prims);
+  else if (s->variant == RT_VAR_BVH_LOCKSTEP)
+    ov = rtk::lane_loop_lockstep<false>(*s->P, g, c, W, s->P->prims);
+  else
+    ov = rtk::lane_loop_bvh(*s->P, g, c, W, s->P->prims);
+  if (ov)
     s->overflow = 1;
   for (int i = 0; i < 4; ++i) s->cnt[i] += rt_emu::counters[i];
   return nullptr;
@@ -84,7 +91,7 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
   P.n_media = H.n_media;
   for (int k = 0; k < H.n_media; ++k) P.media[k] = H.media[k];
   for (int k = 0; k <= RT_MAX_MEDIA; ++k) P.flat_sets[k] = H.flat_sets[k];
-  P.stack_depth = H.flat ? 0 : (H.max_depth > 1 ? H.max_depth : 1);
+  P.stack_depth = H.max_depth > 1 ? H.max_depth : 1;
   P.n_prims = H.n_prims;
   rt_host_plan_work(P, 4096);
   if (chunk > 0) {
@@ -99,6 +106,7 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
   for (auto& f : flags) f = 0;
   Shared s;
   s.P = &P;
+  s.variant = rt_host_variant(H.flat, H.n_media);
   s.accum = &accum;
   s.flags = &flags;
   for (auto& c : s.cnt) c = 0;
