@@ -154,6 +154,30 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   for (int k = 0; k < sc->n_media; ++k)
     if (sets[k + 1].empty()) return fail(err, RT_E_INVALID, "medium %d has an empty boundary", k);
 
+  // media whose boundary is, leaf for leaf in depth-first order, the surface set (DevMedium)
+  std::vector<int> alias(sc->n_media, 0);
+  {
+    std::vector<std::vector<int>> by_set(n_sets);
+    for (int i = 0; i < sc->n_prims; ++i) by_set[sc->prims[i].set].push_back(i);
+    for (auto& v : by_set)
+      std::stable_sort(v.begin(), v.end(), [&](int x, int y) { return sc->prims[x].order < sc->prims[y].order; });
+    auto same = [&](const rt_prim& a, const rt_prim& b) {
+      if (a.kind != b.kind || a.motion != b.motion || a.gid != b.gid || a.uvframe != b.uvframe) return false;
+      for (int j = 0; j < 9; ++j)
+        if (a.p[j] != b.p[j]) return false;
+      return true;
+    };
+    for (int k = 0; k < sc->n_media; ++k) {
+      const auto& a = by_set[0];
+      const auto& b = by_set[k + 1];
+      bool eq = !a.empty() && a.size() == b.size();
+      for (size_t j = 0; eq && j < a.size(); ++j) eq = same(sc->prims[a[j]], sc->prims[b[j]]);
+      alias[k] = eq ? 1 : 0;
+    }
+  }
+  if (const char* e = std::getenv("RT_AMD_NO_ALIAS"))  // experiments: always traverse boundaries
+    if (atoi(e)) std::fill(alias.begin(), alias.end(), 0);
+
   // one BVH per set; primitives stored in leaf order, set after set
   std::vector<int> order;
   std::vector<int> roots(n_sets), set_begin(n_sets + 1, 0);
@@ -277,7 +301,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     S.media[k].neg_inv_density = (float)(-(1.0 / sc->media[k].density));
     S.media[k].material = sc->media[k].material;
     S.media[k].root = roots[k + 1];
-    S.media[k].pad = 0;
+    S.media[k].alias_surface = alias[k];
   }
   S.n_nodes = (int)(S.nodes.size() / 16);
   S.n_prims = n;

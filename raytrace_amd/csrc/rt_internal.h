@@ -69,8 +69,14 @@ struct DevMedium {
   float neg_inv_density;  // -(1 / density)  (Geometry.hs:303)
   int material;
   int root;               // BVH root of the boundary set
-  int pad;
+  int alias_surface;      // 1: the boundary set is geometrically the surface set (see below)
 };
+// alias_surface: the classic volume idiom `dielectric shape` + `constantMedium d shape` (the
+// reference's pawnTest, test/Main.hs:323-344) has a boundary identical to the visible surfaces,
+// leaf for leaf in the same depth-first order.  Then the boundary's first hit on (tmin, inf) IS
+// the surface query's hit (same t, same winning leaf), and the entering case never needs the
+// second query: t1 equals the surface t, so `t1 < tmax` fails (Geometry.hs:313).  The kernel
+// reuses the surface result instead of traversing the boundary again; results are identical.
 
 // Flat scenes (every set one leaf): a set's primitives are grouped by class so the kernel runs
 // one specialised, branch-free loop per class: [first, end_quad) static parallelograms,

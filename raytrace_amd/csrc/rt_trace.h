@@ -795,7 +795,12 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
       // constantMedium (Geometry.hs:306-328)
       const DevMedium& M = P.media[m];
       Closest C1 = no_hit();
-      closest<kFlat>(P, prims, M.root, m + 1, R, kTmin, C1, TW, &overflow);
+      if (M.alias_surface) {  // the boundary is the surface set: its first hit is the surface hit
+        C1.t = C.t;
+        C1.prim = C.prim;
+      } else {
+        closest<kFlat>(P, prims, M.root, m + 1, R, kTmin, C1, TW, &overflow);
+      }
       if (C1.prim < 0) continue;
       const float t1 = C1.t;
       float lo, hi;
@@ -853,7 +858,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
   trav_begin(S, RT_EMPTY_ROOT, kTmin);
   // query sequencing within a segment: q = 0 surfaces; q = 1 + 2m / 2 + 2m medium m, 1st / 2nd hit
   int q = 0, best = -1, hit_medium = -1;
-  float tbest = kInf, t1 = 0.0f;
+  float tbest = kInf, t1 = 0.0f, t_surf = kInf;
   for (;;) {
     // ---- front end: items, samples, segment starts (lanes not tracing)
     const bool need = state == ST_NEED_ITEM;
@@ -894,7 +899,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
         if (trav_done(S)) {
           int next_m = -1;  // medium whose first query starts next
           if (q == 0) {
-            tbest = S.C.t;
+            tbest = t_surf = S.C.t;
             best = S.C.prim;
             next_m = 0;
           } else {
@@ -916,6 +921,12 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
             } else if (S.C.prim >= 0) {  // exit hit of medium m
               medium_event(P, m, I.pix, I.sample, seg, t1, S.C.t, tbest, hit_medium);
             }
+          }
+          // media whose boundary is the surface set reuse the surface hit (DevMedium)
+          while (next_m >= 0 && next_m < P.n_media && P.media[next_m].alias_surface) {
+            if (best >= 0 && !prim_front(P, prims, best, R, t_surf))
+              medium_event(P, next_m, I.pix, I.sample, seg, kTmin, t_surf, tbest, hit_medium);
+            ++next_m;
           }
           if (next_m >= 0) {
             if (next_m < P.n_media) {

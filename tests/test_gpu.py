@@ -119,6 +119,14 @@ def test_kernel_variants_bitwise_identical(gpu, monkeypatch, name):
         assert np.array_equal(img, imgs[0], equal_nan=True)
 
 
+def test_medium_boundary_alias_is_exact(gpu, monkeypatch):
+    cs, world, seed = scenes.pawn_fog(width=96, spp=8)
+    a = R.raytrace(cs, world, seed)
+    monkeypatch.setenv("RT_AMD_NO_ALIAS", "1")
+    b = R.raytrace(cs, world, seed)
+    assert np.array_equal(a, b, equal_nan=True)
+
+
 def test_deterministic_and_shard_invariant(gpu):
     from raytrace_amd.ray import assemble_shards, render_shard
     cs, world, seed = scenes.cornell_box(spp=4, width=50)

@@ -141,6 +141,18 @@ def test_kernel_variants_render_bitwise_identical_images(emu_mod, monkeypatch, n
         assert np.array_equal(img, imgs[0], equal_nan=True)
 
 
+@pytest.mark.parametrize("variant", ["1", "2"])
+def test_medium_boundary_alias_is_exact(emu_mod, monkeypatch, variant):
+    """pawnTest's medium boundary is the dielectric surface itself; reusing the surface hit
+    instead of traversing the boundary (DevMedium.alias_surface) gives the identical image."""
+    cs, world, seed = scenes.pawn_fog(width=48, spp=4)
+    monkeypatch.setenv("RT_AMD_VARIANT", variant)
+    a = emu_mod.render(cs, world, seed)
+    monkeypatch.setenv("RT_AMD_NO_ALIAS", "1")
+    b = emu_mod.render(cs, world, seed)
+    assert np.array_equal(a, b, equal_nan=True)
+
+
 def test_philox_and_splitmix_modes_agree_statistically(oracle_mod):
     """The device's direct samplers (Philox mode) and the reference's rejection samplers
     (splitmix mode) estimate the same image."""
