@@ -309,7 +309,8 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
 }
 
 int rt_host_variant(bool flat, int n_media) {
-  int v = flat ? RT_VAR_FLAT : (n_media > 0 ? RT_VAR_BVH_LOCKSTEP : RT_VAR_BVH);
+  (void)n_media;  // the decoupled loop measured faster with and without media
+  int v = flat ? RT_VAR_FLAT : RT_VAR_BVH;
   if (const char* e = std::getenv("RT_AMD_VARIANT")) {
     const int f = atoi(e);
     if (!flat && (f == RT_VAR_BVH_LOCKSTEP || f == RT_VAR_BVH)) v = f;  // flat scenes run on any variant

@@ -37,8 +37,8 @@
 
 // render-kernel variants (rt_kernel.hip)
 #define RT_VAR_FLAT 0          // every set one flat leaf, lockstep lane loop
-#define RT_VAR_BVH_LOCKSTEP 1  // BVH, lockstep lane loop (scenes with media)
-#define RT_VAR_BVH 2           // BVH, traversal decoupled from shading (no media)
+#define RT_VAR_BVH_LOCKSTEP 1  // BVH, lockstep lane loop (reference schedule; experiments and tests)
+#define RT_VAR_BVH 2           // BVH, traversal decoupled from shading (default for BVH scenes)
 // host choice of variant (rt_build.cpp); env RT_AMD_VARIANT overrides for experiments
 int rt_host_variant(bool flat, int n_media);
 

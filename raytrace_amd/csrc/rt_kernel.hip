@@ -72,10 +72,10 @@ struct AtomicCommit {
 // Variants (rt_internal.h RT_VAR_*), chosen per scene by the host:
 //  RT_VAR_FLAT: every primitive set is one flat leaf; no LDS: the records are read with
 //    wave-uniform addresses (scalar loads into SGPRs, scalar-cache resident); lockstep loop.
-//  RT_VAR_BVH_LOCKSTEP / RT_VAR_BVH: BVH scenes; dynamic LDS = the lanes' traversal stacks
-//    [depth][lane] followed by the top P.lds_nodes nodes.  Scenes without media use the
-//    decoupled loop (traversal and shading interleaved per lane, rt_trace.h lane_loop_bvh);
-//    scenes with media the lockstep loop, whose per-segment query chain stays coherent.
+//  RT_VAR_BVH / RT_VAR_BVH_LOCKSTEP: BVH scenes; dynamic LDS = the lanes' traversal stacks
+//    [depth][lane] followed by the top P.lds_nodes nodes.  The default decouples traversal
+//    from shading per lane (rt_trace.h lane_loop_bvh); the lockstep loop runs every query of a
+//    segment with the whole wave (kept for experiments; images are bit-identical).
 // Register budget: occupancy floor (waves per SIMD).  Flat: 5 (measured 7% faster on the Cornell
 // box than the compiler's default of 4; it now fits 6 unforced).  BVH: 5 (96 VGPRs; faster
 // than 4 on the bunny, pawn and demo1 scenes).

@@ -896,7 +896,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
       if (n_tr < n_live && n_tr * 100 <= n_live * P.trav_exit_pct) break;
       if (tr) {
         trav_round(P, R, S, TW, overflow);
-        if (trav_done(S)) {
+        while (trav_done(S)) {
           int next_m = -1;  // medium whose first query starts next
           if (q == 0) {
             tbest = t_surf = S.C.t;
@@ -936,6 +936,9 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
               state = ST_SHADE;
             }
           }
+          // a query over a set that is a single leaf (e.g. a fog sphere) is tested right away
+          if (state != ST_TRACE || S.node != RT_EMPTY_ROOT) break;
+          trav_round(P, R, S, TW, overflow);
         }
       }
     }
