@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 /* status codes */
 #define RT_OK 0
@@ -64,6 +64,12 @@ extern "C" {
 /* texture kinds (Texture.hs:18-78) */
 #define RT_TEX_CONSTANT 0     /* c0 */
 #define RT_TEX_CHECKER 1      /* nu, nv, c0, c1 */
+#define RT_TEX_IMAGE 2        /* nu = width, nv = height, image = first texel in rt_scene.texels
+                                 (row-major, row 0 = top of the image, 3 floats per texel) */
+#define RT_TEX_NOISE 3        /* nu = layers; params[0] = frequency, params[1..3] = shift; c0, c1
+                                 (fractal Perlin noise, needs rt_scene.perlin) */
+#define RT_TEX_MARBLE 4       /* params[0..2] = stripe direction, params[3] = frequency,
+                                 params[4..6] = shift (turbulence, needs rt_scene.perlin) */
 
 /* background kinds (cs_background restricted to reifiable closures) */
 #define RT_BG_CONST 0         /* c0 */
@@ -98,11 +104,18 @@ typedef struct rt_material {
 
 typedef struct rt_texture {
   int32_t kind;      /* RT_TEX_* */
-  int32_t nu, nv;    /* checker dimensions */
-  int32_t image;     /* reserved (-1) */
+  int32_t nu, nv;    /* checker dimensions | image width, height | noise layers */
+  int32_t image;     /* image: index of its first texel in rt_scene.texels, else -1 */
   double c0[3], c1[3];
-  double params[8];  /* reserved */
+  double params[8];  /* noise / marble parameters (see RT_TEX_*) */
 } rt_texture;
+
+/* The Perlin tables of Noise.hs:21-92: the three fixed permutations (permX/Y/Z) and the 256
+   gradients (`replicateM 256 randomUnitVector` evaluated with mkStdGen 666). */
+typedef struct rt_perlin {
+  int32_t perm[3][256];
+  double grad[256][3];
+} rt_perlin;
 
 typedef struct rt_motion {
   double v0[3], v1[3];   /* world-space shift (1 - time) v0 + time v1 */
@@ -119,6 +132,8 @@ typedef struct rt_scene {
   int32_t n_textures;   const rt_texture* textures;
   int32_t n_motions;    const rt_motion* motions;
   int32_t n_uvframes;   const rt_uvframe* uvframes;
+  int32_t n_texels;     const float* texels;      /* image textures' linear RGB, 3 floats each */
+  const rt_perlin* perlin;                        /* required by noise / marble textures   */
 } rt_scene;
 
 typedef struct rt_redirect_target {   /* cs_redirectTargets element (p, q, u, v) */

@@ -42,8 +42,9 @@ def lib():
         L.oracle_render.restype = ctypes.c_int
         L.oracle_render.argtypes = [P, P, ctypes.c_int, ctypes.c_int, P, P, P, P, P, P, P, P, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, P, ctypes.c_int, ctypes.c_int,
-                                    P, P]
+                                    P, P, P, P, P]
         L.oracle_philox.argtypes = [P, P, P]
+        L.oracle_perlin_gradients.argtypes = [P]
         _lib = L
     return _lib
 
@@ -99,11 +100,21 @@ def render(cs, world, seed, mode=RNG_PHILOX, pixels=None, nthreads=None, variant
         mat_i[k, 1] = m["texture"]
         mat_d[k, 0] = m["param"]
     tex_i = np.zeros((max(len(t.textures), 1), 4), np.int32)
-    tex_d = np.zeros((max(len(t.textures), 1), 6), np.float64)
+    tex_d = np.zeros((max(len(t.textures), 1), 14), np.float64)
     for k, x in enumerate(t.textures):
-        tex_i[k, :3] = [x["kind"], x["nu"], x["nv"]]
+        tex_i[k] = [x["kind"], x["nu"], x["nv"], x["image"]]
         tex_d[k, 0:3] = x["c0"]
         tex_d[k, 3:6] = x["c1"]
+        tex_d[k, 6:14] = x["params"]
+    texels = np.ascontiguousarray(t.texels, dtype=np.float32).reshape(-1, 3)
+    if len(texels) == 0:
+        texels = np.zeros((1, 3), np.float32)
+    if t.perlin is not None:
+        perm = np.ascontiguousarray(t.perlin[0]["perm"], dtype=np.int32)
+        grad = np.ascontiguousarray(t.perlin[0]["grad"], dtype=np.float64)
+    else:
+        perm = np.zeros((3, 256), np.int32)
+        grad = np.zeros((256, 3), np.float64)
     if mode == RNG_SPLITMIX:
         sa, sb = seed.seed, seed.gamma
     else:
@@ -114,7 +125,8 @@ def render(cs, world, seed, mode=RNG_PHILOX, pixels=None, nthreads=None, variant
     nd = np.ascontiguousarray(t.node_d)
     rc = lib().oracle_render(_ptr(ni), _ptr(nd), len(ni), t.root, _ptr(t.children), _ptr(mat_i), _ptr(mat_d),
                              _ptr(tex_i), _ptr(tex_d), _ptr(cam_d), _ptr(cam_i), _ptr(tg), mode, variant, sa, sb,
-                             _ptr(pixels), len(pixels), nthreads, _ptr(out), _ptr(cnt))
+                             _ptr(pixels), len(pixels), nthreads, _ptr(out), _ptr(cnt), _ptr(texels), _ptr(perm),
+                             _ptr(grad))
     if rc < 0:
         raise RuntimeError(f"oracle_render failed: {rc}")
     res = out.reshape(h, w, 3) if full else out
@@ -134,3 +146,10 @@ def philox(ctr, key):
 if __name__ == "__main__":
     build(force="-B" in sys.argv)
     print(LIB_PATH)
+
+
+def perlin_gradients():
+    """The oracle's restatement of Noise.hs:94-98 (256 x 3)."""
+    out = np.zeros((256, 3), np.float64)
+    lib().oracle_perlin_gradients(_ptr(out))
+    return out

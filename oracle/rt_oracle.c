@@ -13,7 +13,8 @@
  *   sphere, sphereUV, planeShape, parallelogram, triangle ...... src/Graphics/Ray/Geometry.hs:58-176
  *   constantMedium, group, bvhNode, transform, moving .......... src/Graphics/Ray/Geometry.hs:298-456
  *   the ten materials ....... src/Graphics/Ray/Material.hs:41-129
- *   constant/checker textures src/Graphics/Ray/Texture.hs:18-53
+ *   textures (constant, checker, image, noise, marble) src/Graphics/Ray/Texture.hs:18-78
+ *   Perlin noise, fractal noise, turbulence ..... src/Graphics/Ray/Noise.hs:15-53
  *
  * The scene arrives as the reference's own geometry TREE (group / bvhNode / transform /
  * moving / constantMedium / `<$` nodes over sphere and planeShape leaves), serialized by
@@ -56,7 +57,7 @@ enum { P_PARALLELOGRAM = 0, P_TRIANGLE = 1 };
 enum { M_LIGHT = 0, M_BLACK = 1, M_LAMBERT = 2, M_LOMMEL = 3, M_MIRROR = 4, M_METAL = 5, M_DIELECTRIC = 6,
        M_TRANSPARENT = 7, M_ISOTROPIC = 8, M_ANISOTROPIC = 9 };
 /* texture kinds */
-enum { T_CONSTANT = 0, T_CHECKER = 1 };
+enum { T_CONSTANT = 0, T_CHECKER = 1, T_IMAGE = 2, T_NOISE = 3, T_MARBLE = 4 };
 /* background kinds */
 enum { BG_CONST = 0, BG_LERPY = 1 };
 
@@ -200,6 +201,21 @@ static v3 random_unit_vector_sm(rng_t* r) {
   }
 }
 
+/* Noise.hs:94-98 gradients = evalState (replicateM 256 randomUnitVector) (mkStdGen 666):
+   the oracle's own restatement, used by the tests to check the product's table. */
+void oracle_perlin_gradients(double* out /* 256 x 3 */) {
+  rng_t r;
+  memset(&r, 0, sizeof r);
+  r.mode = ORACLE_RNG_SPLITMIX;
+  oracle_mkstdgen(666, &r.seed, &r.gamma);
+  for (int k = 0; k < 256; ++k) {
+    v3 g = random_unit_vector_sm(&r);
+    out[3 * k] = g.x;
+    out[3 * k + 1] = g.y;
+    out[3 * k + 2] = g.z;
+  }
+}
+
 /* ------------------------------------------------------------------ scene */
 typedef struct {
   double p, remprob_unused;
@@ -217,6 +233,9 @@ typedef struct {
   const double* md;
   const int32_t* ti;
   const double* td;
+  const float* texels;      /* image textures: 3 floats per texel */
+  const int32_t* perm;      /* Perlin permX / permY / permZ, 3 x 256 */
+  const double* grad;       /* Perlin gradients, 256 x 3 */
   int root;
   /* camera */
   int width, height, spp, max_depth, bg_kind;
@@ -441,16 +460,76 @@ static int hit_node(const scene_t* s, tctx_t* tc, int idx, double time, ray_t ra
   return 0;
 }
 
-/* Texture.hs:18-19, 45-53 */
+/* Noise.hs:15-16 smoothstep */
+static double smoothstep_hs(double x) { return x * x * (3 - 2 * x); }
+
+/* Noise.hs:21-45 perlinNoise: the list comprehension over i, j, k in {0, 1}, summed left to right */
+static double perlin_noise(const scene_t* s, v3 p) {
+  long ix = (long)floor(p.x), iy = (long)floor(p.y), iz = (long)floor(p.z);
+  double fx = p.x - (double)ix, fy = p.y - (double)iy, fz = p.z - (double)iz;
+  double sum = 0;
+  for (int i = 0; i <= 1; ++i)
+    for (int j = 0; j <= 1; ++j)
+      for (int k = 0; k <= 1; ++k) {
+        double di = i, dj = j, dk = k;
+        int g = s->perm[(ix + i) & 255] ^ s->perm[256 + ((iy + j) & 255)] ^ s->perm[512 + ((iz + k) & 255)];
+        v3 grad = mk(s->grad[3 * g], s->grad[3 * g + 1], s->grad[3 * g + 2]);
+        v3 rel = mk(fx - di, fy - dj, fz - dk);
+        double coef = smoothstep_hs(di * fx + (1 - di) * (1 - fx)) * smoothstep_hs(dj * fy + (1 - dj) * (1 - fy)) *
+                      smoothstep_hs(dk * fz + (1 - dk) * (1 - fz));
+        sum = sum + coef * dot(grad, rel);
+      }
+  return sum;
+}
+
+/* Noise.hs:48-53 fractalNoise: sum (take depth (zipWith (*) coefs (map perlinNoise points))) */
+static double fractal_noise(const scene_t* s, int depth, v3 p) {
+  double sum = 0, coef = 1;
+  for (int l = 0; l < depth; ++l) {
+    sum = sum + coef * perlin_noise(s, p);
+    coef = coef / 2;
+    p = smul(2, p);
+  }
+  return sum;
+}
+
+/* Texture.hs:18-78 */
 static v3 eval_texture(const scene_t* s, int tex, const hit_t* h) {
   const int32_t* ti = s->ti + (size_t)tex * 4;
-  const double* td = s->td + (size_t)tex * 6;
+  const double* td = s->td + (size_t)tex * 14;
+  const double* prm = td + 6;
   v3 c0 = mk(td[0], td[1], td[2]);
-  if (ti[0] == T_CONSTANT) return c0;
   v3 c1 = mk(td[3], td[4], td[5]);
-  long i = (long)floor(h->u * (double)ti[1]);
-  long j = (long)floor(h->v * (double)ti[2]);
-  return ((i + j) & 1) == 0 ? c0 : c1;
+  switch (ti[0]) {
+    case T_CONSTANT: return c0;
+    case T_CHECKER: {
+      long i = (long)floor(h->u * (double)ti[1]);
+      long j = (long)floor(h->v * (double)ti[2]);
+      return ((i + j) & 1) == 0 ? c0 : c1;
+    }
+    case T_IMAGE: {  /* Texture.hs:31-41: floor(u w) `mod` w, floor((1 - v) h) `mod` h, image ! (j :. i) */
+      long w = ti[1], hh = ti[2];
+      long i = (long)floor(h->u * (double)w) % w, j = (long)floor((1 - h->v) * (double)hh) % hh;
+      if (i < 0) i += w;
+      if (j < 0) j += hh;
+      const float* t = s->texels + 3 * ((size_t)ti[3] + (size_t)j * w + i);
+      return mk(t[0], t[1], t[2]);
+    }
+    case T_NOISE: {  /* Texture.hs:56-67 */
+      double scale = 0.5 / 0.8;
+      v3 q = add(smul(prm[0], h->p), mk(prm[1], prm[2], prm[3]));
+      double n = fractal_noise(s, ti[1], q) * scale + 0.5;
+      v3 diff = sub(c1, c0);
+      return add(c0, smul(n, diff));
+    }
+    default: {  /* T_MARBLE, Texture.hs:70-78 */
+      double freq = prm[3];
+      double sin_arg = freq * dot(mk(prm[0], prm[1], prm[2]), h->p);
+      double noise = 10 * fabs(fractal_noise(s, 7, add(smul(0.25 * freq, h->p), mk(prm[4], prm[5], prm[6]))));
+      double m = 0.5 + 0.5 * sin(sin_arg + noise);
+      return mk(m, m, m);
+    }
+  }
 }
 
 /* rt_hit of a redirect target: parallelogram hit on (0, infinity) (Ray.hs:143-145) */
@@ -687,11 +766,12 @@ int oracle_render(const int32_t* node_i, const double* node_d, int n_nodes, int 
                   const int32_t* mat_i, const double* mat_d, const int32_t* tex_i, const double* tex_d,
                   const double* cam_d, const int32_t* cam_i, const double* targets, int rng_mode, int variant,
                   uint64_t seed_a, uint64_t seed_b, const int32_t* pixels, int n_pixels, int nthreads, double* out_rgb,
-                  double* counters) {
+                  double* counters, const float* texels, const int32_t* perlin_perm, const double* perlin_grad) {
   if (root < 0 || root >= n_nodes) return -1;
   scene_t s;
   memset(&s, 0, sizeof s);
   s.ni = node_i; s.nd = node_d; s.children = children; s.mi = mat_i; s.md = mat_d; s.ti = tex_i; s.td = tex_d;
+  s.texels = texels; s.perm = perlin_perm; s.grad = perlin_grad;
   s.root = root;
   s.width = cam_i[0]; s.spp = cam_i[1]; s.max_depth = cam_i[2]; s.bg_kind = cam_i[3]; s.nt = cam_i[4];
   s.rng_mode = rng_mode; s.variant = variant;

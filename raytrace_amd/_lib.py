@@ -44,6 +44,8 @@ class RtScene(ctypes.Structure):
         ("n_textures", ctypes.c_int32), ("textures", ctypes.c_void_p),
         ("n_motions", ctypes.c_int32), ("motions", ctypes.c_void_p),
         ("n_uvframes", ctypes.c_int32), ("uvframes", ctypes.c_void_p),
+        ("n_texels", ctypes.c_int32), ("texels", ctypes.c_void_p),
+        ("perlin", ctypes.c_void_p),
     ]
 
 
@@ -87,7 +89,7 @@ def load():
     L.rt_encode8_async.argtypes = [P, P, ctypes.c_int64, ctypes.c_int32, P]
     for name in EXPORTED:
         getattr(L, name)
-    if L.rt_abi_version() != 1:
+    if L.rt_abi_version() != 2:
         raise RtDeviceError("librt_amd.so ABI version mismatch")
     _lib = L
     return L
@@ -148,6 +150,9 @@ def scene_struct(flat):
     s.n_textures, s.textures = len(flat.textures), ptr(flat.textures)
     s.n_motions, s.motions = len(flat.motions), ptr(flat.motions)
     s.n_uvframes, s.uvframes = len(flat.uvframes), ptr(flat.uvframes)
+    texels = np.ascontiguousarray(flat.texels, dtype=np.float32).reshape(-1, 3)
+    s.n_texels, s.texels = len(texels), ptr(texels)
+    s.perlin = ptr(flat.perlin) if flat.perlin is not None else None
     s._keep = keep
     return s
 

@@ -55,6 +55,9 @@ struct rt_device_scene {
   DevTexture* texs = nullptr;
   float* motions = nullptr;
   float* uvframes = nullptr;
+  float* texels = nullptr;
+  int* perlin_perm = nullptr;
+  float* perlin_grad = nullptr;
   int* flat_prim = nullptr;
   int* status = nullptr;
   int surface_root = RT_EMPTY_ROOT;
@@ -104,6 +107,9 @@ int rt_scene_destroy(rt_device_scene* s) {
   (void)hipFree(s->texs);
   (void)hipFree(s->motions);
   (void)hipFree(s->uvframes);
+  (void)hipFree(s->texels);
+  (void)hipFree(s->perlin_perm);
+  (void)hipFree(s->perlin_grad);
   (void)hipFree(s->flat_prim);
   (void)hipFree(s->status);
   delete s;
@@ -129,6 +135,8 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
       (rc = upload(&s->prim_mat, H.prim_mat)) || (rc = upload(&s->prim_uv, H.prim_uv)) ||
       (rc = upload(&s->mats, H.mats)) || (rc = upload(&s->texs, H.texs)) || (rc = upload(&s->motions, H.motions)) ||
       (rc = upload(&s->uvframes, H.uvframes)) || (rc = upload(&s->flat_prim, H.flat_prim)) ||
+      (rc = upload(&s->texels, H.texels)) || (rc = upload(&s->perlin_perm, H.perlin_perm)) ||
+      (rc = upload(&s->perlin_grad, H.perlin_grad)) ||
       (rc = upload(&s->status, status))) {
     rt_scene_destroy(s);
     return rc;
@@ -141,8 +149,8 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
   s->n_prims = H.n_prims;
   s->max_depth = H.max_depth;
   s->stack_depth = H.max_depth > 1 ? H.max_depth : 1;
-  s->variant = rt_host_variant(H.flat, H.n_media);
-  if (s->variant != RT_VAR_FLAT) {
+  s->variant = rt_host_variant(H.flat, H.n_media, H.noise);
+  if ((s->variant & RT_VAR_BASE) != RT_VAR_FLAT) {
     // stage as many top (breadth-first) surface nodes as fit beside the stacks in the per-
     // workgroup budget; env RT_AMD_LDS_NODES caps it (0 disables, for experiments)
     const int room = (RT_LDS_WG_BUDGET - s->stack_depth * RT_BLOCK * (int)sizeof(int)) / 64;
@@ -184,6 +192,9 @@ int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint
   P.texs = s->texs;
   P.motions = s->motions;
   P.uvframes = s->uvframes;
+  P.texels = s->texels;
+  P.perlin_perm = s->perlin_perm;
+  P.perlin_grad = s->perlin_grad;
   P.flat_prim = s->flat_prim;
   P.status = s->status;
   P.out = d_out_rgb;

@@ -89,11 +89,30 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   if ((sc->n_prims && !sc->prims) || (sc->n_media && !sc->media) || (sc->n_materials && !sc->materials) ||
       (sc->n_textures && !sc->textures) || (sc->n_motions && !sc->motions) || (sc->n_uvframes && !sc->uvframes))
     return fail(err, RT_E_INVALID, "null array with nonzero count");
+  if (sc->n_texels < 0 || (sc->n_texels && !sc->texels)) return fail(err, RT_E_INVALID, "bad texel array");
+  bool need_perlin = false;
   for (int i = 0; i < sc->n_textures; ++i) {
     const rt_texture& t = sc->textures[i];
-    if (t.kind != RT_TEX_CONSTANT && t.kind != RT_TEX_CHECKER)
+    if (t.kind < RT_TEX_CONSTANT || t.kind > RT_TEX_MARBLE)
       return fail(err, RT_E_UNSUPPORTED, "texture %d: kind %d is not evaluated on the device", i, t.kind);
     if (!finite_n(t.c0, 3) || !finite_n(t.c1, 3)) return fail(err, RT_E_INVALID, "texture %d: non-finite colour", i);
+    if (!finite_n(t.params, 8)) return fail(err, RT_E_INVALID, "texture %d: non-finite parameters", i);
+    if (t.kind == RT_TEX_IMAGE &&
+        (t.nu <= 0 || t.nv <= 0 || t.image < 0 || (long long)t.image + (long long)t.nu * t.nv > sc->n_texels))
+      return fail(err, RT_E_INVALID, "texture %d: image %dx%d at texel %d exceeds the %d texels", i, t.nu, t.nv,
+                  t.image, sc->n_texels);
+    if (t.kind == RT_TEX_NOISE && t.nu < 0) return fail(err, RT_E_INVALID, "texture %d: negative noise layers", i);
+    if (t.kind == RT_TEX_NOISE || t.kind == RT_TEX_MARBLE) need_perlin = true;
+  }
+  S.noise = need_perlin;
+  if (need_perlin) {
+    if (!sc->perlin) return fail(err, RT_E_INVALID, "noise / marble textures need rt_scene.perlin");
+    for (int a = 0; a < 3; ++a)
+      for (int k = 0; k < 256; ++k)
+        if (sc->perlin->perm[a][k] < 0 || sc->perlin->perm[a][k] > 255)
+          return fail(err, RT_E_INVALID, "perlin permutation entry out of [0, 255]");
+    for (int k = 0; k < 256; ++k)
+      if (!finite_n(sc->perlin->grad[k], 3)) return fail(err, RT_E_INVALID, "non-finite perlin gradient");
   }
   for (int i = 0; i < sc->n_materials; ++i) {
     const rt_material& m = sc->materials[i];
@@ -280,10 +299,23 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     d.kind = t.kind;
     d.nu = t.nu;
     d.nv = t.nv;
+    d.off = t.kind == RT_TEX_IMAGE ? t.image : 0;
     for (int a = 0; a < 3; ++a) {
       d.c0[a] = (float)t.c0[a];
       d.c1[a] = (float)t.c1[a];
     }
+    for (int a = 0; a < 8; ++a) d.prm[a] = (float)t.params[a];
+  }
+  S.texels.assign((size_t)sc->n_texels * 4, 0.0f);
+  for (int i = 0; i < sc->n_texels; ++i)
+    for (int a = 0; a < 3; ++a) S.texels[4 * (size_t)i + a] = sc->texels[3 * (size_t)i + a];
+  S.perlin_perm.assign(3 * 256, 0);
+  S.perlin_grad.assign(256 * 4, 0.0f);
+  if (sc->perlin) {
+    for (int a = 0; a < 3; ++a)
+      for (int k = 0; k < 256; ++k) S.perlin_perm[256 * a + k] = sc->perlin->perm[a][k];
+    for (int k = 0; k < 256; ++k)
+      for (int a = 0; a < 3; ++a) S.perlin_grad[4 * k + a] = (float)sc->perlin->grad[k][a];
   }
   S.motions.assign((size_t)sc->n_motions * 8, 0.0f);
   for (int i = 0; i < sc->n_motions; ++i)
@@ -308,7 +340,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   return RT_OK;
 }
 
-int rt_host_variant(bool flat, int n_media) {
+int rt_host_variant(bool flat, int n_media, bool noise) {
   (void)n_media;  // the decoupled loop measured faster with and without media
   int v = flat ? RT_VAR_FLAT : RT_VAR_BVH;
   if (const char* e = std::getenv("RT_AMD_VARIANT")) {
@@ -316,7 +348,7 @@ int rt_host_variant(bool flat, int n_media) {
     if (!flat && (f == RT_VAR_BVH_LOCKSTEP || f == RT_VAR_BVH)) v = f;  // flat scenes run on any variant
     if (flat && f >= RT_VAR_FLAT && f <= RT_VAR_BVH) v = f;
   }
-  return v;
+  return v | (noise ? RT_VAR_NOISE : 0);
 }
 
 int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex, KernelParams& P,

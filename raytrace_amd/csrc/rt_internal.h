@@ -39,8 +39,10 @@
 #define RT_VAR_FLAT 0          // every set one flat leaf, lockstep lane loop
 #define RT_VAR_BVH_LOCKSTEP 1  // BVH, lockstep lane loop (reference schedule; experiments and tests)
 #define RT_VAR_BVH 2           // BVH, traversal decoupled from shading (default for BVH scenes)
-// host choice of variant (rt_build.cpp); env RT_AMD_VARIANT overrides for experiments
-int rt_host_variant(bool flat, int n_media);
+#define RT_VAR_BASE 3
+#define RT_VAR_NOISE 4         // flag: the scene has noise / marble textures (their code compiled in)
+// host choice of variant (rt_build.cpp); env RT_AMD_VARIANT overrides the base for experiments
+int rt_host_variant(bool flat, int n_media, bool noise);
 
 #define RT_KIND_MASK 3
 #define RT_FLAG_MOTION 4
@@ -59,10 +61,11 @@ struct DevMaterial {
 };
 
 struct DevTexture {
-  int kind, nu, nv, pad;
+  int kind, nu, nv, off;  // RT_TEX_*; checker dims | image width, height, first texel | noise layers
   float c0[3];
   float c1[3];
-  float pad2[2];
+  float prm[8];           // noise: freq, shift.xyz | marble: dir.xyz, freq, shift.xyz
+  float pad[2];
 };
 
 struct DevMedium {
@@ -120,6 +123,9 @@ struct KernelParams {
   const DevTexture* texs;
   const float* motions;    // 8 floats per motion: v0.xyz, -, v1.xyz, -
   const float* uvframes;   // 12 floats per frame: rows of R (xyz, -)
+  const float* texels;     // image textures: 4 floats per texel (linear RGB, -)
+  const int* perlin_perm;  // 3 x 256 permutation entries (Noise.hs permX / permY / permZ)
+  const float* perlin_grad;  // 256 gradients, 4 floats each (xyz, -)
   const int* flat_prim;    // flat scenes: closest-hit slot -> primitive index (DevFlatSet)
   float* out;
   int* status;             // device word: nonzero on stack overflow
@@ -150,7 +156,8 @@ struct KernelParams {
 
 // Host-side scene image, ready for upload (rt_build.cpp).
 struct HostScene {
-  std::vector<float> nodes, prims, prim_uv, motions, uvframes;
+  std::vector<float> nodes, prims, prim_uv, motions, uvframes, texels, perlin_grad;
+  std::vector<int> perlin_perm;
   std::vector<int> prim_mat;
   std::vector<int> flat_prim;  // flat scenes: slot -> primitive index
   std::vector<DevMaterial> mats;
@@ -162,6 +169,7 @@ struct HostScene {
   int n_nodes = 0, n_prims = 0, max_depth = 0;
   int surface_nodes = 0;  // nodes of the surface BVH: [0, surface_nodes), breadth-first
   bool flat = false;  // every set is a single flat leaf (no BVH nodes)
+  bool noise = false;  // some texture is a noise / marble texture
 };
 
 struct rt_scene;

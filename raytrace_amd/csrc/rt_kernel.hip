@@ -85,7 +85,7 @@ struct AtomicCommit {
 #ifndef RT_WAVES_BVH
 #define RT_WAVES_BVH 5
 #endif
-template <int kVar>
+template <int kVar, bool kNoise>
 __global__ __launch_bounds__(RT_BLOCK)
 __attribute__((amdgpu_waves_per_eu(kVar == RT_VAR_FLAT ? RT_WAVES_FLAT : RT_WAVES_BVH)))
 void rt_render_kernel(KernelParams P) {
@@ -94,7 +94,7 @@ void rt_render_kernel(KernelParams P) {
   AtomicCommit commit{P.accum, P.nanflag};
   int overflow;
   if constexpr (kVar == RT_VAR_FLAT) {
-    overflow = rtk::lane_loop_lockstep<true>(P, grab, commit, rtk::Trav{nullptr, 0, nullptr}, P.prims);
+    overflow = rtk::lane_loop_lockstep<true, kNoise>(P, grab, commit, rtk::Trav{nullptr, 0, nullptr}, P.prims);
   } else {
     // LDS: [stack_depth][RT_BLOCK] stack words, then the top P.lds_nodes BVH nodes (64 B each)
     rtk::v4* lds_nodes = reinterpret_cast<rtk::v4*>(smem + P.stack_depth * RT_BLOCK);
@@ -106,9 +106,9 @@ void rt_render_kernel(KernelParams P) {
     __syncthreads();
     const rtk::Trav W{smem + threadIdx.x, RT_BLOCK, lds_nodes};
     if constexpr (kVar == RT_VAR_BVH_LOCKSTEP)
-      overflow = rtk::lane_loop_lockstep<false>(P, grab, commit, W, P.prims);
+      overflow = rtk::lane_loop_lockstep<false, kNoise>(P, grab, commit, W, P.prims);
     else
-      overflow = rtk::lane_loop_bvh(P, grab, commit, W, P.prims);
+      overflow = rtk::lane_loop_bvh<kNoise>(P, grab, commit, W, P.prims);
   }
   if (overflow) atomicOr(P.status, 1);
 }
@@ -163,20 +163,26 @@ __global__ __launch_bounds__(256) void rt_encode8_kernel(const float* __restrict
 }
 
 static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
-  return variant == RT_VAR_FLAT ? 0 : (size_t)stack_depth * RT_BLOCK * sizeof(int) + (size_t)lds_nodes * 64;
+  return (variant & RT_VAR_BASE) == RT_VAR_FLAT ? 0
+                                                 : (size_t)stack_depth * RT_BLOCK * sizeof(int) + (size_t)lds_nodes * 64;
 }
 
-template <int kVar>
-static hipError_t occupancy(int* per_cu, size_t lds) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, rt_render_kernel<kVar>, RT_BLOCK, lds);
+// the kernel instantiation of a variant code (base variant | RT_VAR_NOISE)
+typedef void (*render_fn)(KernelParams);
+static render_fn render_kernel_of(int variant) {
+  const bool noise = (variant & RT_VAR_NOISE) != 0;
+  switch (variant & RT_VAR_BASE) {
+    case RT_VAR_FLAT: return noise ? rt_render_kernel<RT_VAR_FLAT, true> : rt_render_kernel<RT_VAR_FLAT, false>;
+    case RT_VAR_BVH_LOCKSTEP:
+      return noise ? rt_render_kernel<RT_VAR_BVH_LOCKSTEP, true> : rt_render_kernel<RT_VAR_BVH_LOCKSTEP, false>;
+    default: return noise ? rt_render_kernel<RT_VAR_BVH, true> : rt_render_kernel<RT_VAR_BVH, false>;
+  }
 }
 
 int rt_render_resident_blocks(int device, int stack_depth, int variant, int lds_nodes) {
   int per_cu = 0, cus = 0;
   size_t lds = render_lds_bytes(stack_depth, variant, lds_nodes);
-  hipError_t e = variant == RT_VAR_FLAT            ? occupancy<RT_VAR_FLAT>(&per_cu, lds)
-                 : variant == RT_VAR_BVH_LOCKSTEP ? occupancy<RT_VAR_BVH_LOCKSTEP>(&per_cu, lds)
-                                                   : occupancy<RT_VAR_BVH>(&per_cu, lds);
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_kernel_of(variant), RT_BLOCK, lds);
   if (e != hipSuccess) return -1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return -1;
   if (per_cu < 1) per_cu = 1;
@@ -188,13 +194,7 @@ int rt_launch_render(const KernelParams& p, int grid_blocks, int variant, void* 
   long long need = ((long long)p.n_items + RT_BLOCK - 1) / RT_BLOCK;
   int grid = need < grid_blocks ? (int)need : grid_blocks;
   size_t lds = render_lds_bytes(p.stack_depth, variant, p.lds_nodes);
-  hipStream_t st = (hipStream_t)stream;
-  if (variant == RT_VAR_FLAT)
-    hipLaunchKernelGGL(rt_render_kernel<RT_VAR_FLAT>, dim3(grid), dim3(RT_BLOCK), lds, st, p);
-  else if (variant == RT_VAR_BVH_LOCKSTEP)
-    hipLaunchKernelGGL(rt_render_kernel<RT_VAR_BVH_LOCKSTEP>, dim3(grid), dim3(RT_BLOCK), lds, st, p);
-  else
-    hipLaunchKernelGGL(rt_render_kernel<RT_VAR_BVH>, dim3(grid), dim3(RT_BLOCK), lds, st, p);
+  hipLaunchKernelGGL(render_kernel_of(variant), dim3(grid), dim3(RT_BLOCK), lds, (hipStream_t)stream, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -27,6 +27,7 @@
 #pragma once
 #include <stdint.h>
 
+#include "../../include/rt.h"
 #include "rt_internal.h"
 
 #ifdef RT_HOST_EMU
@@ -367,13 +368,75 @@ RT_FN HitInfo surface_info(const KernelParams& P, cfp prims, int pi, const RayCt
   return h;
 }
 
-RT_FN f3 eval_texture(const KernelParams& P, int tex, float u, float v) {
-  const RT_CAS DevTexture* T = (const RT_CAS DevTexture*)P.texs + tex;
+// Perlin noise (Noise.hs:21-45): gradients at the 8 lattice corners, smoothstep weights.
+// Kept compact (corner loop not unrolled) so the rarely used noise textures do not raise the
+// register allocation of the whole lane loop.
+RT_FN float smooth3(float x) { return x * x * (3.0f - 2.0f * x); }
+RT_FN float perlin_noise(const RT_CAS int* perm, cfp grad, f3 p) {
+  const float x0 = floorf(p.x), y0 = floorf(p.y), z0 = floorf(p.z);
+  const int ix = (int)x0, iy = (int)y0, iz = (int)z0;
+  const float fx = p.x - x0, fy = p.y - y0, fz = p.z - z0;
+  float sum = 0.0f;
+#pragma unroll 1
+  for (int c = 0; c < 8; ++c) {
+    const int i = c >> 2, j = (c >> 1) & 1, k = c & 1;
+    const int g = perm[(ix + i) & 255] ^ perm[256 + ((iy + j) & 255)] ^ perm[512 + ((iz + k) & 255)];
+    const float rx = fx - (float)i, ry = fy - (float)j, rz = fz - (float)k;
+    const float w = smooth3(i ? fx : 1.0f - fx) * smooth3(j ? fy : 1.0f - fy) * smooth3(k ? fz : 1.0f - fz);
+    sum += w * dot(ldc3(grad + 4 * g), mk3(rx, ry, rz));
+  }
+  return sum;
+}
+// fractalNoise (Noise.hs:48-53): layers of doubling frequency and halving weight
+RT_FN float fractal_noise(const RT_CAS int* perm, cfp grad, int depth, f3 p) {
+  float sum = 0.0f, w = 1.0f;
+#pragma unroll 1
+  for (int l = 0; l < depth; ++l) {
+    sum += w * perlin_noise(perm, grad, p);
+    w *= 0.5f;
+    p = 2.0f * p;
+  }
+  return sum;
+}
+// Solid noise textures.  Their register needs (lattice corners per octave, on top of the live
+// path state) would raise the allocation of the whole lane loop, so they are compiled only into
+// the kernel instantiations for scenes that use them (template flag kNoise, host-selected).
+RT_FN f3 eval_noise_texture(const RT_CAS int* perm, cfp grad, const RT_CAS DevTexture* T, f3 p) {
   f3 c0 = f3{T->c0[0], T->c0[1], T->c0[2]};
-  if (T->kind == 0) return c0;
-  // checkerTexture (Texture.hs:45-53)
-  int i = (int)floorf(u * (float)T->nu), j = (int)floorf(v * (float)T->nv);
-  return ((i + j) & 1) == 0 ? c0 : f3{T->c1[0], T->c1[1], T->c1[2]};
+  if (T->kind == RT_TEX_NOISE) {  // noiseTexture (Texture.hs:56-67)
+    const f3 q = T->prm[0] * p + mk3(T->prm[1], T->prm[2], T->prm[3]);
+    const float n = fractal_noise(perm, grad, T->nu, q) * (0.5f / 0.8f) + 0.5f;
+    return c0 + n * (f3{T->c1[0], T->c1[1], T->c1[2]} - c0);
+  }
+  // marbleTexture (Texture.hs:70-78)
+  const float freq = T->prm[3];
+  const float arg = freq * dot(mk3(T->prm[0], T->prm[1], T->prm[2]), p);
+  const float turb =
+      fabsf(fractal_noise(perm, grad, 7, (0.25f * freq) * p + mk3(T->prm[4], T->prm[5], T->prm[6])));
+  const float m = 0.5f + 0.5f * sinf(arg + 10.0f * turb);
+  return mk3(m, m, m);
+}
+
+// Textures (Texture.hs:18-78); (u, v) for uv textures, the hit point p for solid ones
+template <bool kNoise>
+RT_FN f3 eval_texture(const KernelParams& P, int tex, float u, float v, f3 p) {
+  const RT_CAS DevTexture* T = (const RT_CAS DevTexture*)P.texs + tex;
+  const int kind = T->kind;
+  f3 c0 = f3{T->c0[0], T->c0[1], T->c0[2]};
+  if (kind == RT_TEX_CONSTANT) return c0;
+  if (kind == RT_TEX_CHECKER) {  // checkerTexture (Texture.hs:45-53)
+    int i = (int)floorf(u * (float)T->nu), j = (int)floorf(v * (float)T->nv);
+    return ((i + j) & 1) == 0 ? c0 : f3{T->c1[0], T->c1[1], T->c1[2]};
+  }
+  if (kind == RT_TEX_IMAGE) {  // imageTexture (Texture.hs:31-41): wrap, v = 0 at the bottom row
+    const int w = T->nu, h = T->nv;
+    int i = (int)floorf(u * (float)w) % w, j = (int)floorf((1.0f - v) * (float)h) % h;
+    i += i < 0 ? w : 0;
+    j += j < 0 ? h : 0;
+    return ldc3(cf(P.texels) + 4 * ((size_t)T->off + (size_t)j * w + i));
+  }
+  if constexpr (kNoise) return eval_noise_texture((const RT_CAS int*)P.perlin_perm, cf(P.perlin_grad), T, p);
+  return c0;  // not reached: scenes with noise textures run the kNoise kernels
 }
 
 // rt_hit of a redirect target: parallelogram on (0, infinity) (Ray.hs:143-145)
@@ -596,6 +659,7 @@ RT_FN void medium_event(const KernelParams& P, int m, uint32_t pix, int sample, 
 // One rayColor level after the closest hit (Ray.hs:176-224): background on a miss, else the
 // material of the surface / medium hit.  Updates L, T and, when the path continues, the ray
 // (and seg).  Returns true when the path terminates.
+template <bool kNoise>
 RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int& seg, float tbest, int best,
                  int hit_medium, RayCtx& R, f3& L, f3& T) {
   RT_HOOK_SEGMENT(pix, sample, seg, R, tbest, best, hit_medium, L, T);
@@ -624,25 +688,29 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
   }
   const RT_CAS DevMaterial* Mp = (const RT_CAS DevMaterial*)P.mats + h.mat;
   const DevMaterial Mt = DevMaterial{Mp->kind, Mp->tex, Mp->param, 0};
+  // the material's texture, evaluated once (every material but pitchBlack and dielectric reads
+  // it; one inlined copy of the texture code keeps the register allocation down)
+  f3 tex = mk3(0.f, 0.f, 0.f);
+  if (Mt.kind != RT_MAT_PITCH_BLACK && Mt.kind != RT_MAT_DIELECTRIC) tex = eval_texture<kNoise>(P, Mt.tex, h.u, h.v, h.p);
   u4 w = philox(pix, (uint32_t)sample, (uint32_t)seg, RT_EV_SCATTER, P.key0, P.key1);
   const bool last = seg + 1 >= P.cam.max_depth;  // rayColor (depth - 1) with depth - 1 <= 0 is zero
   f3 newdir = R.d;
   switch (Mt.kind) {
     case 0:  // lightSource: emit, Absorb
-      L = L + T * eval_texture(P, Mt.tex, h.u, h.v);
+      L = L + T * tex;
       terminate = true;
       break;
     case 1:  // pitchBlack
       terminate = true;
       break;
     case 4:  // mirror
-      T = T * eval_texture(P, Mt.tex, h.u, h.v);
+      T = T * tex;
       newdir = unit(reflect(h.n, R.d));
       break;
     case 5: {  // metal
       f3 d2 = reflect(h.n, R.d) + Mt.param * unit_vector(w.y, w.z);
       if (dot(d2, h.n) > 0.0f) {
-        T = T * eval_texture(P, Mt.tex, h.u, h.v);
+        T = T * tex;
         newdir = normalize(d2);
       } else {
         terminate = true;
@@ -667,7 +735,7 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
       break;
     }
     case 7:  // transparent
-      T = T * eval_texture(P, Mt.tex, h.u, h.v);
+      T = T * tex;
       break;
     default: {  // 2 lambertian, 3 lommelSeeliger (HemisphereF); 8 isotropic, 9 anisotropic (SphereF)
       const bool hemi = Mt.kind == 2 || Mt.kind == 3;
@@ -700,7 +768,7 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
           mix += P.targets[k].prob * (tt * tt * RT_RCP(fabsf(dot(ld3(P.targets[k].cr), dir))));
       }
       float pdf = P.rem_prob * pdf1 + mix;
-      f3 f = eval_texture(P, Mt.tex, h.u, h.v);
+      f3 f = tex;
       if (Mt.kind == 3) {
         float mu0 = -dot(R.d, h.n), mu1 = dot(dir, h.n);
         f = (0.25f * RT_RCP(mu0 + mu1)) * f;
@@ -751,7 +819,7 @@ RT_FN bool open_item(const KernelParams& P, int item, ItemCtx& I) {
 // for lanes with need == true.  `commit(tile_pixel, sx, sy, sz, bad)` adds a finished item's
 // sums.  One segment per iteration, all of its queries run by the whole wave together: the flat
 // kernel (every lane tests the same primitives) and the BVH kernel of scenes with media.
-template <bool kFlat, class Grab, class Commit>
+template <bool kFlat, bool kNoise, class Grab, class Commit>
 RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW,
                              const float* prims_) {
   const cfp prims = cf(prims_);
@@ -817,7 +885,7 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
       }
       medium_event(P, m, I.pix, I.sample, seg, lo, hi, tbest, hit_medium);
     }
-    if (shade(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T)) {
+    if (shade<kNoise>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T)) {
       RT_HOOK_SAMPLE(I.pix, I.sample, L);
       sx += to_fixed(L.x, bad);
       sy += to_fixed(L.y, bad);
@@ -840,7 +908,7 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
 // entering it, the second (Geometry.hs:306-328) — each starting inside the traversal loop as
 // soon as the previous one finishes.
 enum : int { ST_NEED_ITEM = 0, ST_NEED_SAMPLE = 1, ST_START_SEG = 2, ST_TRACE = 3, ST_SHADE = 4 };
-template <class Grab, class Commit>
+template <bool kNoise, class Grab, class Commit>
 RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW, const float* prims_) {
   const cfp prims = cf(prims_);
   int overflow = 0;
@@ -944,7 +1012,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
     }
     // ---- shade the segments whose queries are complete
     if (state == ST_SHADE) {
-      if (shade(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T)) {
+      if (shade<kNoise>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T)) {
         RT_HOOK_SAMPLE(I.pix, I.sample, L);
         sx += to_fixed(L.x, bad);
         sy += to_fixed(L.y, bad);

@@ -85,13 +85,16 @@ class _Tables:
             a[i]["param"] = m.param
         return a
 
-    def texture_array(self, check_device: bool):
+    def texture_array(self):
+        """(rt_texture records, texels float32 (n, 3), rt_perlin record or None)."""
         a = np.zeros(len(self.textures), TEXTURE_DTYPE)
+        texels = []
+        n_texels = 0
+        need_perlin = False
         for i, t in enumerate(self.textures):
-            if check_device and t.kind not in (M.TEX_CONSTANT, M.TEX_CHECKER):
-                what = {M.TEX_IMAGE: "imageTexture", M.TEX_NOISE: "noiseTexture", M.TEX_MARBLE: "marbleTexture",
-                        M.TEX_CLOSURE: "solidTexture/uvTexture closure"}[t.kind]
-                raise RtUnsupported(f"{what} is not evaluated on the device (constantTexture / checkerTexture are)")
+            if t.kind == M.TEX_CLOSURE:
+                raise RtUnsupported("solidTexture / uvTexture closures are not reifiable for the device "
+                                    "(constant, checker, image, noise and marble textures are)")
             a[i]["kind"] = t.kind
             a[i]["nu"] = t.nu
             a[i]["nv"] = t.nv
@@ -100,17 +103,32 @@ class _Tables:
             a[i]["c1"] = t.c1
             p = list(t.params)[:8]
             a[i]["params"][: len(p)] = p
-        return a
+            if t.kind == M.TEX_IMAGE:
+                img = np.ascontiguousarray(t.image, dtype=np.float32).reshape(t.image.shape[0], t.image.shape[1], 3)
+                h, w = img.shape[:2]
+                a[i]["nu"], a[i]["nv"], a[i]["image"] = w, h, n_texels
+                texels.append(img.reshape(-1, 3))
+                n_texels += h * w
+            elif t.kind in (M.TEX_NOISE, M.TEX_MARBLE):
+                need_perlin = True
+        tex = np.concatenate(texels) if texels else np.zeros((0, 3), np.float32)
+        perlin = None
+        if need_perlin:
+            from .perlin import perlin_record
+            perlin = perlin_record()
+        return a, tex, perlin
 
 
 class FlatScene:
     """Flattened scene: numpy record arrays with the exact layout of include/rt.h."""
 
-    def __init__(self, prims, media, materials, textures, motions, uvframes, n_surface):
+    def __init__(self, prims, media, materials, textures, motions, uvframes, n_surface, texels=None, perlin=None):
         self.prims = prims
         self.media = media
         self.materials = materials
         self.textures = textures
+        self.texels = texels if texels is not None else np.zeros((0, 3), np.float32)
+        self.perlin = perlin
         self.motions = motions
         self.uvframes = uvframes
         self.n_surface = n_surface
@@ -256,7 +274,8 @@ def flatten(world: G.Geometry) -> FlatScene:
     for k, r in enumerate(uvframes):
         uvf[k]["r"] = r
     n_surface = int(np.sum(prims["set"] == 0)) if len(prims) else 0
-    return FlatScene(prims, med, tabs.material_array(), tabs.texture_array(check_device=True), mot, uvf, n_surface)
+    tex, texels, perlin = tabs.texture_array()
+    return FlatScene(prims, med, tabs.material_array(), tex, mot, uvf, n_surface, texels, perlin)
 
 
 M_SPHERE_KIND = PRIM_SPHERE
@@ -267,7 +286,9 @@ NI, ND = 4, 30
 
 
 class SerializedTree:
-    def __init__(self, node_i, node_d, children, root, materials, textures, n_media):
+    def __init__(self, node_i, node_d, children, root, materials, textures, n_media, texels=None, perlin=None):
+        self.texels = texels if texels is not None else np.zeros((0, 3), np.float32)
+        self.perlin = perlin
         self.node_i = node_i
         self.node_d = node_d
         self.children = children
@@ -344,5 +365,5 @@ def serialize_tree(world: G.Geometry) -> SerializedTree:
     ni = np.array(node_i, dtype=np.int32).reshape(-1, NI)
     nd = np.array(node_d, dtype=np.float64).reshape(-1, ND)
     ch = np.array(children if children else [0], dtype=np.int32)
-    return SerializedTree(ni, nd, ch, root, tabs.material_array(), tabs.texture_array(check_device=False),
-                          media_count[0])
+    tex, texels, perlin = tabs.texture_array()
+    return SerializedTree(ni, nd, ch, root, tabs.material_array(), tex, media_count[0], texels, perlin)

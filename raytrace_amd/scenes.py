@@ -17,8 +17,8 @@ from .camera import constBackground, defaultCameraSettings, grayFade, sky
 from .core import V3, degrees, mkStdGen, midpoint, norm, sub
 from .geometry import (boundingBox, bvhTree, cuboid, constantMedium, group, parallelogram, pureGeometry, readObj,
                        rotateY, scale, sphere, transform, transformVertices, translate, triangleMesh)
-from .material import (checkerTexture, constantTexture, dielectric, isotropic, lambertian, lightSource, metal,
-                       mirror)
+from .material import (checkerTexture, constantTexture, dielectric, isotropic, lambertian, lightSource,
+                       marbleTexture, metal, mirror, noiseTexture)
 from .core import fromCorners
 
 DATA_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data")
@@ -170,6 +170,19 @@ def pawn_fog(width=800, spp=2000, depth=20):
     return settings, _pawn_world(mesh, fog=True), mkStdGen(55)
 
 
+def noise_test(width=400, spp=100, depth=50, seed=7):
+    """noiseTest (test/Main.hs:63-86): a Perlin-noise ground sphere and a marble ball.  The
+    reference seeds it with newStdGen; this build fixes `seed`."""
+    world = group([
+        lambertian(noiseTexture(2, 2.0, V3(10, 0, 0), 0, 1)) << sphere(V3(0, -1000, 0), 1000),
+        lambertian(marbleTexture(V3(0, 0, 1), 4, 0)) << sphere(V3(0, 2, 0), 2),
+    ])
+    settings = defaultCameraSettings(cs_aspectRatio=16 / 9, cs_imageWidth=width, cs_samplesPerPixel=spp,
+                                     cs_maxRecursionDepth=depth, cs_background=sky, cs_vfov=degrees(20),
+                                     cs_center=V3(13, 2, 3), cs_lookAt=V3(0, 0, 0))
+    return settings, world, mkStdGen(seed)
+
+
 CONFIGS = {
     "readme": readme_scene,
     "cornell": cornell_box,
@@ -177,4 +190,5 @@ CONFIGS = {
     "bunny_cornell": bunny_cornell,
     "pawn_fog": pawn_fog,
     "pawn_test": pawn_test,
+    "noise_test": noise_test,
 }

@@ -52,12 +52,20 @@ void* worker(void* arg) {
   Commit c{s};
   const rtk::Trav W{stack.data(), 1, nullptr};  // the emulator reads every node from memory
   int ov = 0;
-  if (s->variant == RT_VAR_FLAT)
-    ov = rtk::lane_loop_lockstep<true>(*s->P, g, c, W, s->P->prims);
-  else if (s->variant == RT_VAR_BVH_LOCKSTEP)
-    ov = rtk::lane_loop_lockstep<false>(*s->P, g, c, W, s->P->prims);
-  else
-    ov = rtk::lane_loop_bvh(*s->P, g, c, W, s->P->prims);
+  const bool noise = (s->variant & RT_VAR_NOISE) != 0;
+  switch (s->variant & RT_VAR_BASE) {
+    case RT_VAR_FLAT:
+      ov = noise ? rtk::lane_loop_lockstep<true, true>(*s->P, g, c, W, s->P->prims)
+                 : rtk::lane_loop_lockstep<true, false>(*s->P, g, c, W, s->P->prims);
+      break;
+    case RT_VAR_BVH_LOCKSTEP:
+      ov = noise ? rtk::lane_loop_lockstep<false, true>(*s->P, g, c, W, s->P->prims)
+                 : rtk::lane_loop_lockstep<false, false>(*s->P, g, c, W, s->P->prims);
+      break;
+    default:
+      ov = noise ? rtk::lane_loop_bvh<true>(*s->P, g, c, W, s->P->prims)
+                 : rtk::lane_loop_bvh<false>(*s->P, g, c, W, s->P->prims);
+  }
   if (ov)
     s->overflow = 1;
   for (int i = 0; i < 4; ++i) s->cnt[i] += rt_emu::counters[i];
@@ -85,6 +93,9 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
   P.texs = H.texs.data();
   P.motions = H.motions.data();
   P.uvframes = H.uvframes.data();
+  P.texels = H.texels.data();
+  P.perlin_perm = H.perlin_perm.data();
+  P.perlin_grad = H.perlin_grad.data();
   P.flat_prim = H.flat_prim.data();
   P.out = out;
   P.surface_root = H.surface_root;
@@ -106,7 +117,7 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
   for (auto& f : flags) f = 0;
   Shared s;
   s.P = &P;
-  s.variant = rt_host_variant(H.flat, H.n_media);
+  s.variant = rt_host_variant(H.flat, H.n_media, H.noise);
   s.accum = &accum;
   s.flags = &flags;
   for (auto& c : s.cnt) c = 0;

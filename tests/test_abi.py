@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
     exported = set(re.findall(r"\bT (rt_\w+)", out.stdout))
     assert set(names) <= exported
-    assert L.rt_abi_version() == 1
+    assert L.rt_abi_version() == 2
 
 
 def test_host_only_entry_points_without_gpu():
@@ -59,7 +59,8 @@ int main(void) {
   P(rt_material); O(rt_material, param);
   P(rt_texture); O(rt_texture, c0); O(rt_texture, params);
   P(rt_motion); P(rt_uvframe);
-  P(rt_scene); O(rt_scene, prims); O(rt_scene, uvframes);
+  P(rt_scene); O(rt_scene, prims); O(rt_scene, uvframes); O(rt_scene, texels); O(rt_scene, perlin);
+  P(rt_perlin); O(rt_perlin, grad);
   P(rt_camera_settings); O(rt_camera_settings, image_width); O(rt_camera_settings, background_c0);
   O(rt_camera_settings, defocus_angle); O(rt_camera_settings, redirect_targets);
   P(rt_redirect_target); P(rt_exec); P(rt_stats); O(rt_stats, samples);
@@ -87,6 +88,9 @@ def test_record_layouts_match_header():
     assert c["rt_motion"] == S.MOTION_DTYPE.itemsize and c["rt_uvframe"] == S.UVFRAME_DTYPE.itemsize
     assert c["rt_scene"] == ctypes.sizeof(_lib.RtScene)
     assert c["rt_scene.uvframes"] == _lib.RtScene.uvframes.offset
+    assert c["rt_scene.texels"] == _lib.RtScene.texels.offset and c["rt_scene.perlin"] == _lib.RtScene.perlin.offset
+    from raytrace_amd.perlin import PERLIN_DTYPE
+    assert c["rt_perlin"] == PERLIN_DTYPE.itemsize and c["rt_perlin.grad"] == PERLIN_DTYPE.fields["grad"][1]
     assert c["rt_camera_settings"] == ctypes.sizeof(_lib.RtCameraSettings)
     for f in ("image_width", "background_c0", "defocus_angle", "redirect_targets"):
         assert c[f"rt_camera_settings.{f}"] == getattr(_lib.RtCameraSettings, f).offset, f

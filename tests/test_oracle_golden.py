@@ -9,10 +9,13 @@ within 1.5x the seed-to-seed noise floor measured for the same config (tests/gol
 noise_floor.json), and global means within 1 %.  The decoded images pass through the reference
 writers' exact 8-bit quantisation (clipping at 1 included) before comparison.
 """
+import os
+
 import numpy as np
 import pytest
 
-from conftest import as_published, block8, pixel_agreement
+import raytrace_amd as R
+from conftest import GOLDEN, as_published, block8, pixel_agreement
 from raytrace_amd import scenes
 from raytrace_amd.camera import image_height
 
@@ -151,6 +154,51 @@ def test_medium_boundary_alias_is_exact(emu_mod, monkeypatch, variant):
     monkeypatch.setenv("RT_AMD_NO_ALIAS", "1")
     b = emu_mod.render(cs, world, seed)
     assert np.array_equal(a, b, equal_nan=True)
+
+
+def test_perlin_tables(oracle_mod):
+    """The product's Perlin tables: three permutations of 0..255 (Noise.hs:60-92) and the 256
+    gradients of Noise.hs:94-98, identical to the oracle's independent C restatement."""
+    from raytrace_amd import perlin
+    perm = perlin.permutations()
+    assert perm.shape == (3, 256)
+    for row in perm:
+        assert sorted(row.tolist()) == list(range(256))
+    g = perlin.gradients()
+    assert np.array_equal(g, oracle_mod.perlin_gradients())
+    assert np.allclose((g * g).sum(1), 1.0, atol=1e-12)
+
+
+def test_textured_scenes_kernel_logic_matches_oracle(oracle_mod, emu_mod):
+    """Noise / marble (noiseTest, test/Main.hs:63-86) and image textures: the kernel's source
+    built for the host against the oracle, per pixel."""
+    img = np.load(os.path.join(GOLDEN, "earthmap_128x64.npy")).astype(np.float32)
+    tex = R.imageTexture(img)
+    image_world = R.group([R.lambertian(tex) << R.sphere((0, 0, -2), 0.6),
+                           R.lambertian(tex) << R.parallelogram((-2, -1, -3), (4, 0, 0), (0, 2.5, 0)),
+                           R.lambertian(R.constantTexture(0.5)) << R.sphere((0, -100.6, -2), 100)])
+    cases = [scenes.noise_test(width=96, spp=4),
+             (R.defaultCameraSettings(cs_imageWidth=80, cs_samplesPerPixel=4, cs_background=R.sky), image_world,
+              R.mkStdGen(3))]
+    for cs, world, seed in cases:
+        got = emu_mod.render(cs, world, seed)
+        ref = oracle_mod.render(cs, world, seed, mode=oracle_mod.RNG_PHILOX)
+        assert np.isfinite(got).all()
+        assert pixel_agreement(got, ref) >= 0.99
+        np.testing.assert_allclose(got.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=5e-3)
+
+
+def test_image_texture_lookup_wraps_and_flips(oracle_mod):
+    """imageTexture (Texture.hs:31-41): (u, v) = (0, 0) is the bottom-left texel, coordinates
+    wrap.  A camera looking straight at a unit quad textured with a 2 x 2 image of four
+    colours sees them in image order (row 0 at the top)."""
+    img = np.array([[[1, 0, 0], [0, 1, 0]], [[0, 0, 1], [1, 1, 0]]], np.float32)
+    world = R.lightSource(R.imageTexture(img)) << R.parallelogram((-1, -1, -1), (2, 0, 0), (0, 2, 0))
+    cs = R.defaultCameraSettings(cs_imageWidth=4, cs_aspectRatio=1.0, cs_samplesPerPixel=1,
+                                 cs_vfov=2 * np.arctan(0.5), cs_center=(0, 0, 1), cs_lookAt=(0, 0, 0))
+    out = oracle_mod.render(cs, world, R.mkStdGen(1), mode=oracle_mod.RNG_PHILOX)
+    assert np.allclose(out[0, 0], [1, 0, 0]) and np.allclose(out[0, 3], [0, 1, 0])
+    assert np.allclose(out[3, 0], [0, 0, 1]) and np.allclose(out[3, 3], [1, 1, 0])
 
 
 def test_philox_and_splitmix_modes_agree_statistically(oracle_mod):
