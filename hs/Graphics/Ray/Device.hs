@@ -29,8 +29,14 @@ import qualified Data.Massiv.Array as A
 import qualified Data.Massiv.Array.Unsafe as AU
 import Control.Monad.State (State)
 
--- | Reified textures (Texture.hs:18-53).
-data TextureD = ConstantD Color | CheckerD Int Int Color Color
+-- | Reified textures (Texture.hs:18-78).  Images are row-major linear RGB (row 0 at the top);
+-- noise / marble textures make the flattened scene carry the Perlin tables (rt_perlin:
+-- permX / permY / permZ and Noise.hs's `gradients`).
+data TextureD
+  = ConstantD Color | CheckerD Int Int Color Color
+  | ImageD (A.Matrix A.U Color)
+  | NoiseD Int Double (V3 Double) Color Color     -- ^ layers, frequency, shift, colour 0, colour 1
+  | MarbleD Vec3 Double (V3 Double)               -- ^ stripe direction, frequency, shift
 
 -- | Reified materials (Material.hs:41-129).
 data MaterialD
