@@ -107,6 +107,9 @@ def main():
     ap.add_argument("--row-block", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="gather + assemble + sanity-check the frame after timing")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, the real path); gloo gathers through host memory (N>1 rehearsal on one "
+                         "GPU, with RT_BENCH_ONE_DEVICE=1 mapping every rank to device 0)")
     args = ap.parse_args()
 
     import torch
@@ -122,10 +125,15 @@ def main():
     if world_size != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world_size}; using WORLD_SIZE")
     n = world_size
+    if os.environ.get("RT_BENCH_ONE_DEVICE") == "1":
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if n > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     fn = scenes.CONFIGS[args.config]
     cs, world, seed = fn()
@@ -148,7 +156,12 @@ def main():
             e1.record(stream)
             ev.append((e0, e1))
         if n > 1:
-            dist.all_gather_into_tensor(gathered, tile)
+            if args.dist_backend == "nccl":
+                dist.all_gather_into_tensor(gathered, tile)
+            else:  # rehearsal path: through host memory
+                parts = [torch.empty((rows, w, 3), dtype=torch.float32) for _ in range(n)]
+                dist.all_gather(parts, tile.cpu())
+                gathered.copy_(torch.cat(parts).to(dev))
 
     for _ in range(args.warmup):
         step(False)
@@ -165,7 +178,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if n > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))

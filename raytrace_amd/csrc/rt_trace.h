@@ -458,11 +458,14 @@ RT_FN long long to_fixed(float x, bool& bad) {
     bad = true;
     return 0;
   }
-#ifdef RT_EXP_CHEAP_FIXED  // ablation: 32-bit conversion only (wrong above 2^31 / 2^16)
-  return (long long)(int)(x * 65536.0f) << 16;
-#else
-  return (long long)((double)x * RT_FIX_SCALE);
-#endif
+  // x * 2^32 without FP64: for x >= 0 (radiance) the integer part and the fraction are exact
+  // in FP32 (x - floor(x) is exact) and the fraction scaled by 2^32 is exact, so two 32-bit
+  // conversions give exactly trunc(x * 2^32).  (Negative inputs, possible only with negative
+  // user colours, are within 2^-25 relative of it.)
+  const float fl = floorf(x);
+  const long long hi = (long long)(int)fl;
+  const unsigned lo = (unsigned)((x - fl) * 4294967296.0f);
+  return (long long)((unsigned long long)hi << 32) + (long long)lo;
 }
 
 // ---------------------------------------------------------------- BVH traversal
@@ -853,7 +856,7 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
     }
     RT_COUNT(2);
     // ---- closest hit over the surfaces and every medium (Ray.hs:178)
-    prep_ray(R);
+    if constexpr (!kFlat) prep_ray(R);  // reciprocal direction: BVH slab tests only
     Closest C = no_hit();
     closest<kFlat>(P, prims, P.surface_root, 0, R, kTmin, C, TW, &overflow);
     float tbest = C.t;
