@@ -76,18 +76,22 @@ struct AtomicCommit {
 //    [depth][lane] followed by the top P.lds_nodes nodes.  The default decouples traversal
 //    from shading per lane (rt_trace.h lane_loop_bvh); the lockstep loop runs every query of a
 //    segment with the whole wave (kept for experiments; images are bit-identical).
-// Register budget: occupancy floor (waves per SIMD).  Flat: 5 (measured 7% faster on the Cornell
-// box than the compiler's default of 4; it now fits 6 unforced).  BVH: 5 (96 VGPRs; faster
-// than 4 on the bunny, pawn and demo1 scenes).
+// Register budget: occupancy floor (waves per SIMD).  Flat: 7 (72 VGPRs, no spills; 2.8%
+// faster on the Cornell box than the 6 it fits unforced, 8 spills and is slower); flat with
+// noise textures: 5.  BVH: 5 (96 VGPRs; faster than 4 on the bunny, pawn and demo1 scenes).
 #ifndef RT_WAVES_FLAT
-#define RT_WAVES_FLAT 5
+#define RT_WAVES_FLAT 7
+#endif
+#ifndef RT_WAVES_FLAT_NOISE
+#define RT_WAVES_FLAT_NOISE 5
 #endif
 #ifndef RT_WAVES_BVH
 #define RT_WAVES_BVH 5
 #endif
 template <int kVar, bool kNoise>
 __global__ __launch_bounds__(RT_BLOCK)
-__attribute__((amdgpu_waves_per_eu(kVar == RT_VAR_FLAT ? RT_WAVES_FLAT : RT_WAVES_BVH)))
+__attribute__((amdgpu_waves_per_eu(kVar == RT_VAR_FLAT ? (kNoise ? RT_WAVES_FLAT_NOISE : RT_WAVES_FLAT)
+                                                         : RT_WAVES_BVH)))
 void rt_render_kernel(KernelParams P) {
   extern __shared__ int smem[];
   WaveGrab grab{P.counter, 0, 0};
