@@ -238,18 +238,26 @@ RT_FN void isect_sphere(const PrimRec& r, f3 o, const RayCtx& R, float tmin, flo
   t = self ? 2.0f * h : tn;
   q = fminf(self ? 1.0f : disc, t - tmin_up);
 }
-// planeShape (Geometry.hs:117-144): parallelogram a, b in [0,1]; triangle a, b >= 0, a + b <= 1
-template <bool kQuad>
-RT_FN void isect_plane(const PrimRec& r, f3 o, const RayCtx& R, float tmin_up, bool self, float& t, float& q) {
+// planeShape (Geometry.hs:117-144): parallelogram a, b in [0,1]; triangle a, b >= 0, a + b <= 1.
+// kQuad: 1 parallelogram, 0 triangle, -1 either (per-lane `quad`, a select instead of a branch)
+template <int kQuad>
+RT_FN void isect_plane(const PrimRec& r, f3 o, const RayCtx& R, float tmin_up, bool self, float& t, float& q,
+                       bool quad = false) {
   f3 n = xyz(r.a);
   float denom = dot(n, R.d);
   f3 qo = xyz(r.b) - o;
   t = dot(n, qo) * RT_RCP(denom);
   f3 prel = t * R.d - qo;
   float aa = dot(prel, xyz(r.c)), bb = dot(prel, xyz(r.e));
-  float m1 = kQuad ? fminf(fminf(aa, bb), 1.0f - aa) : fminf(fminf(aa, bb), 1.0f - aa - bb);
-  float m2 = fminf(fabsf(denom) - 1e-8f, t - tmin_up);
-  if (kQuad) m2 = fminf(m2, 1.0f - bb);
+  float m1, m2 = fminf(fabsf(denom) - 1e-8f, t - tmin_up);
+  if constexpr (kQuad < 0) {  // quad: min(1 - a, 1 - b); triangle: 1 - a - b
+    m1 = fminf(fminf(aa, bb), quad ? fminf(1.0f - aa, 1.0f - bb) : 1.0f - aa - bb);
+  } else if constexpr (kQuad == 1) {
+    m1 = fminf(fminf(aa, bb), 1.0f - aa);
+    m2 = fminf(m2, 1.0f - bb);
+  } else {
+    m1 = fminf(fminf(aa, bb), 1.0f - aa - bb);
+  }
   q = self ? -1.0f : fminf(m1, m2);
 }
 // kKeyOnly (flat sets): only the key is tracked; t and the primitive follow from it afterwards
@@ -278,10 +286,12 @@ RT_FN void test_rec(const KernelParams& P, const PrimRec& r, int pi, const RayCt
   float t, q;
   if ((kf & RT_KIND_MASK) == 0)
     isect_sphere(r, o, R, tmin, tmin_up, self, t, q);
-  else if ((kf & RT_KIND_MASK) == 1)
-    isect_plane<true>(r, o, R, tmin_up, self, t, q);
+  else if constexpr (!kKeyOnly)  // BVH leaves: parallelograms and triangles share one path
+    isect_plane<-1>(r, o, R, tmin_up, self, t, q, (kf & RT_KIND_MASK) == 1);
+  else if ((kf & RT_KIND_MASK) == 1)  // flat sets (uniform kind): scalar branch
+    isect_plane<1>(r, o, R, tmin_up, self, t, q);
   else
-    isect_plane<false>(r, o, R, tmin_up, self, t, q);
+    isect_plane<0>(r, o, R, tmin_up, self, t, q);
   consider<kKeyOnly>(C, t, q, RT_F2I(r.c.w), pi);
 }
 
@@ -294,7 +304,7 @@ RT_FN void test_static(const PrimRec& r, const RayCtx& R, float tmin, float tmin
   if constexpr (kKind == RT_PRIM_CLASS_SPHERE)
     isect_sphere(r, R.o, R, tmin, tmin_up, self, t, q);
   else
-    isect_plane<kKind == RT_PRIM_CLASS_QUAD>(r, R.o, R, tmin_up, self, t, q);
+    isect_plane<kKind == RT_PRIM_CLASS_QUAD ? 1 : 0>(r, R.o, R, tmin_up, self, t, q);
   consider<true>(C, t, q, RT_F2I(r.c.w), 0);
 }
 
@@ -531,6 +541,21 @@ RT_FN void trav_round(const KernelParams& P, const RayCtx& R, TravState& S, cons
     float lfar = fminf(fminf(fmaxf(lx0, lx1), fmaxf(ly0, ly1)), fminf(fmaxf(lz0, lz1), S.C.t));
     float rnear = fmaxf(fmaxf(fminf(rx0, rx1), fminf(ry0, ry1)), fmaxf(fminf(rz0, rz1), S.tmin));
     float rfar = fminf(fminf(fmaxf(rx0, rx1), fmaxf(ry0, ry1)), fminf(fmaxf(rz0, rz1), S.C.t));
+#ifdef RT_EXP_DOUBLE_NODE  // ablation: the slab tests computed twice (marginal cost of a node visit)
+    {
+      const float e = (float)P.cam.pad;
+      float ax0 = fmaf(n0.x + e, R.idir.x, -R.oidir.x), ax1 = fmaf(n0.y + e, R.idir.x, -R.oidir.x);
+      float ay0 = fmaf(n0.z + e, R.idir.y, -R.oidir.y), ay1 = fmaf(n0.w + e, R.idir.y, -R.oidir.y);
+      float az0 = fmaf(n2.x + e, R.idir.z, -R.oidir.z), az1 = fmaf(n2.y + e, R.idir.z, -R.oidir.z);
+      float bx0 = fmaf(n1.x + e, R.idir.x, -R.oidir.x), bx1 = fmaf(n1.y + e, R.idir.x, -R.oidir.x);
+      float by0 = fmaf(n1.z + e, R.idir.y, -R.oidir.y), by1 = fmaf(n1.w + e, R.idir.y, -R.oidir.y);
+      float bz0 = fmaf(n2.z + e, R.idir.z, -R.oidir.z), bz1 = fmaf(n2.w + e, R.idir.z, -R.oidir.z);
+      lnear = fminf(lnear, fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fmaxf(fminf(az0, az1), S.tmin)));
+      lfar = fmaxf(lfar, fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fminf(fmaxf(az0, az1), S.C.t)));
+      rnear = fminf(rnear, fmaxf(fmaxf(fminf(bx0, bx1), fminf(by0, by1)), fmaxf(fminf(bz0, bz1), S.tmin)));
+      rfar = fmaxf(rfar, fminf(fminf(fmaxf(bx0, bx1), fmaxf(by0, by1)), fminf(fmaxf(bz0, bz1), S.C.t)));
+    }
+#endif
     const bool hl = lnear <= lfar, hr = rnear <= rfar;
     if (hl && hr) {
       const bool rfirst = rnear < lnear;
@@ -558,6 +583,11 @@ RT_FN void trav_round(const KernelParams& P, const RayCtx& R, TravState& S, cons
     const int first = enc >> RT_LEAF_SHIFT, count = (enc & ((1 << RT_LEAF_SHIFT) - 1)) + 1;
     for (int k = 0; k < count; ++k)
       test_rec(P, ld_rec(cf(P.prims) + 16 * (size_t)(first + k)), first + k, R, S.tmin, S.tmin_up, S.C);
+#ifdef RT_EXP_DOUBLE_LEAF  // ablation: every leaf tested twice (marginal cost of the leaf tests)
+    for (int k = 0; k < count; ++k)
+      test_rec(P, ld_rec(cf(P.prims) + 16 * (size_t)(first + k)), first + k, R, S.tmin,
+               S.tmin_up + (float)P.cam.pad, S.C);
+#endif
     S.leaf = 0;
     if (S.node < 0 && S.node != kDone) {  // the node we stopped at is a leaf too: test it next
       S.leaf = S.node;
