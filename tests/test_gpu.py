@@ -148,6 +148,17 @@ def test_textured_scenes_match_oracle_per_pixel(gpu, oracle_mod, name):
     np.testing.assert_allclose(img.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=5e-3)
 
 
+@pytest.mark.parametrize("kind", ["sphere", "triangle", "parallelogram", "mirror"])
+def test_known_answer_hits(gpu, kind):
+    """The analytic known-answer scenes of test_oracle_golden on the GPU:
+    pixels wholly inside / outside the primitive are exact."""
+    from test_oracle_golden import _kat_scene
+    cs, world, mask = _kat_scene(kind)
+    out = R.raytrace(cs, world, R.mkStdGen(5))
+    m = mask >= 0
+    np.testing.assert_allclose(out[m], np.repeat(mask[m][:, None], 3, axis=1), atol=1e-6)
+
+
 def test_deterministic_and_shard_invariant(gpu):
     from raytrace_amd.ray import assemble_shards, render_shard
     cs, world, seed = scenes.cornell_box(spp=4, width=50)

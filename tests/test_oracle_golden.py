@@ -201,6 +201,71 @@ def test_image_texture_lookup_wraps_and_flips(oracle_mod):
     assert np.allclose(out[3, 0], [0, 0, 1]) and np.allclose(out[3, 3], [1, 1, 0])
 
 
+def _kat_scene(kind):
+    """Analytic known-answer scenes: an emitter of radiance 1 (or a
+    mirror of albedo 0.5 in front of a large emitter) seen head-on by a 16 x 16 camera with a
+    1:1 viewport of half-width 1 at distance 1, background 0.  Returns (world, mask) where
+    mask[j, i] is 1 / 0.5 / 0 for pixels whose whole footprint lies inside / mirrored / outside
+    the primitive (-1: straddles an edge, not checked).  The pixel jitter cannot move a sample out
+    of its pixel footprint, so these pixels are exact whatever the random numbers."""
+    import numpy as np
+    n = 16
+    light = R.lightSource(R.constantTexture(1.0))
+    # pixel (j, i) covers x in [-1 + i/8, -1 + (i+1)/8], y in [1 - (j+1)/8, 1 - j/8] on the z = -1 plane
+    xs0 = -1 + np.arange(n) / 8.0
+    ys1 = 1 - np.arange(n) / 8.0
+    X0, Y1 = np.meshgrid(xs0, ys1)
+    X1, Y0 = X0 + 1 / 8.0, Y1 - 1 / 8.0
+    mask = -np.ones((n, n))
+    if kind == "sphere":   # Geometry.hs:58-94, radius 0.5 at the plane's centre (far side behind)
+        world = light << R.sphere((0, 0, -1.5), 0.5)
+        # conservative: inside if the pixel's rays all hit: angular radius asin(0.5/1.5) ~ 0.3398 at z=-1
+        rr = np.tan(np.arcsin(0.5 / 1.5))
+        far = np.maximum(np.maximum(np.hypot(X0, Y0), np.hypot(X1, Y1)), np.maximum(np.hypot(X0, Y1), np.hypot(X1, Y0)))
+        near = np.hypot(np.clip(0, X0, X1), np.clip(0, Y0, Y1))
+        mask[far < rr - 1e-3] = 1
+        mask[near > rr + 1e-3] = 0
+    elif kind == "triangle":  # planeShape with a, b >= 0, a + b <= 1 (Geometry.hs:117-151)
+        world = light << R.triangle(((-0.5, -0.5, -1), (0, 0)), ((0.5, -0.5, -1), (1, 0)), ((-0.5, 0.5, -1), (0, 1)))
+        inside = lambda x, y: (x >= -0.5) & (y >= -0.5) & (x + y <= 0.0)
+        allin = inside(X0, Y0) & inside(X1, Y0) & inside(X0, Y1) & inside(X1, Y1)
+        anyin = (X1 > -0.5) & (Y1 > -0.5) & (X0 + Y0 < 0.0)
+        mask[allin] = 1
+        mask[~anyin] = 0
+    elif kind == "parallelogram":
+        world = light << R.parallelogram((-0.5, -0.25, -1), (1.0, 0, 0), (0.25, 0.75, 0))
+        def inside(x, y):
+            b = (y + 0.25) / 0.75
+            a = (x + 0.5) - 0.25 * b
+            return (a >= 0) & (a <= 1) & (b >= 0) & (b <= 1)
+        allin = inside(X0, Y0) & inside(X1, Y0) & inside(X0, Y1) & inside(X1, Y1)
+        anyin = inside(X0, Y0) | inside(X1, Y0) | inside(X0, Y1) | inside(X1, Y1) | \
+            ((X1 > -0.5) & (X0 < 0.75) & (Y1 > -0.25) & (Y0 < 0.5) & ~(X1 < -0.5 + 0.25 * (Y0 + 0.25) / 0.75) &
+             ~(X0 > 0.5 + 0.25 * (Y1 + 0.25) / 0.75))
+        mask[allin] = 1
+        mask[~anyin] = 0
+    else:  # mirror (Material.hs:64-67): albedo 0.5 mirror facing the camera, emitter behind the camera
+        world = R.group([R.mirror(R.constantTexture(0.5)) << R.parallelogram((-0.5, -0.5, -1), (1, 0, 0), (0, 1, 0)),
+                         light << R.parallelogram((-10, -10, 5), (0, 20, 0), (20, 0, 0))])
+        allin = (X0 >= -0.5) & (X1 <= 0.5) & (Y0 >= -0.5) & (Y1 <= 0.5)
+        mask[allin] = 0.5
+        mask[(X1 <= -0.5) | (X0 >= 0.5) | (Y1 <= -0.5) | (Y0 >= 0.5)] = 0
+    cs = R.defaultCameraSettings(cs_imageWidth=n, cs_aspectRatio=1.0, cs_samplesPerPixel=4, cs_vfov=np.pi / 2,
+                                 cs_center=(0, 0, 0), cs_lookAt=(0, 0, -1), cs_focusDist=1.0,
+                                 cs_background=R.constBackground(0.0), cs_maxRecursionDepth=5)
+    return cs, world, mask
+
+
+@pytest.mark.parametrize("kind", ["sphere", "triangle", "parallelogram", "mirror"])
+def test_oracle_known_answer_hits(oracle_mod, kind):
+    cs, world, mask = _kat_scene(kind)
+    out = oracle_mod.render(cs, world, R.mkStdGen(5), mode=oracle_mod.RNG_PHILOX)
+    assert out.shape == (16, 16, 3)
+    m = mask >= 0
+    assert m.sum() > 100 and (mask == (0.5 if kind == "mirror" else 1)).sum() > 4
+    np.testing.assert_array_equal(out[m], np.repeat(mask[m][:, None], 3, axis=1))
+
+
 def test_philox_and_splitmix_modes_agree_statistically(oracle_mod):
     """The device's direct samplers (Philox mode) and the reference's rejection samplers
     (splitmix mode) estimate the same image."""
