@@ -428,7 +428,20 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
   return RT_OK;
 }
 
+FastDiv rt_host_fastdiv(uint32_t d) {
+  FastDiv f{0u, 0, d, 0};
+  if (d <= 1) return f;
+  int l = 0;
+  while ((1ull << l) < d) ++l;  // ceil(log2 d)
+  f.m = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+  f.s = l - 1;
+  return f;
+}
+
 void rt_host_plan_work(KernelParams& P, long long resident_lanes) {
+  P.div_tile = rt_host_fastdiv((uint32_t)P.tile_rows * (uint32_t)P.cam.width);
+  P.div_width = rt_host_fastdiv((uint32_t)P.cam.width);
+  P.div_block = rt_host_fastdiv((uint32_t)P.row_block);
   P.trav_exit_pct = 50;
   if (const char* e = std::getenv("RT_AMD_TRAV_PCT")) P.trav_exit_pct = std::max(0, std::min(100, atoi(e)));
   // Items = (tile pixel, chunk of consecutive samples), claimed in pixel order.  Small chunks

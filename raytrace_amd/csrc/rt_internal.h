@@ -114,6 +114,16 @@ struct DevCamera {
   int pad;
 };
 
+// Exact unsigned 32-bit division by a launch-constant divisor (Granlund-Montgomery, round-up
+// multiplier with the add-and-shift fix-up): q = (t + ((n - t) >> 1)) >> s, t = umulhi(n, m).
+// The host computes m, s (rt_build.cpp rt_host_fastdiv); d == 1 is the identity.
+struct FastDiv {
+  uint32_t m;
+  int s;
+  uint32_t d;
+  int pad;
+};
+
 struct KernelParams {
   const float* nodes;      // 16 floats per node
   const float* prims;      // 16 floats per primitive
@@ -150,6 +160,7 @@ struct KernelParams {
   DevCamera cam;
   uint32_t key0, key1;
   int n_shards, shard, row_block, tile_rows;
+  FastDiv div_tile, div_width, div_block;  // tile pixels, image width, row block
 };
 
 #define RT_FIX_SCALE 4294967296.0  // 2^32: per-sample radiance is accumulated as int64 * 2^-32
@@ -193,4 +204,5 @@ int rt_launch_render(const KernelParams& p, int grid_blocks, int variant, void* 
 int rt_launch_resolve(const KernelParams& p, void* stream);
 // work decomposition (rt_build.cpp): chunk so that items >= ~8 x resident lanes
 void rt_host_plan_work(KernelParams& P, long long resident_lanes);
+FastDiv rt_host_fastdiv(uint32_t d);
 int rt_launch_encode8(const float* in, uint8_t* out, int64_t n, int encoding, void* stream);

@@ -135,6 +135,11 @@ RT_FN u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
 #ifndef RT_PHILOX_ROUNDS
 #define RT_PHILOX_ROUNDS 10
 #endif
+#if !defined(RT_HOST_EMU) && !defined(RT_EXP_HOIST_KEYS)
+  // the round keys are two scalar adds per round: recompute them at every call instead of
+  // letting the compiler keep all twenty live (and spilled) across the lane loop
+  asm volatile("" : "+s"(k0), "+s"(k1));
+#endif
 #pragma unroll
   for (int r = 0; r < RT_PHILOX_ROUNDS; ++r) {
     if (r) {
@@ -833,14 +838,22 @@ struct ItemCtx {
   int item, tp, px, gy, sample, s_end;
   uint32_t pix;
 };
+RT_FN uint32_t fast_div(uint32_t n, const FastDiv& f) {
+  if (f.d == 1u) return n;  // uniform
+  const uint32_t t = (uint32_t)(((uint64_t)n * f.m) >> 32);
+  return (t + ((n - t) >> 1)) >> f.s;
+}
 RT_FN bool open_item(const KernelParams& P, int item, ItemCtx& I) {
   const int W = P.cam.width, tile_pixels = P.tile_rows * W;
   I.item = item;
-  const int k = item / tile_pixels;
+  // item, tile pixel and row are non-negative: exact multiply-shift division by the launch
+  // constants instead of the ~20-instruction signed integer division sequences
+  const int k = (int)fast_div((uint32_t)item, P.div_tile);
   I.tp = item - k * tile_pixels;
-  const int tr = I.tp / W;
+  const int tr = (int)fast_div((uint32_t)I.tp, P.div_width);
   I.px = I.tp - tr * W;
-  I.gy = ((tr / P.row_block) * P.n_shards + P.shard) * P.row_block + (tr % P.row_block);
+  const int tb = (int)fast_div((uint32_t)tr, P.div_block);
+  I.gy = (tb * P.n_shards + P.shard) * P.row_block + (tr - tb * P.row_block);
   I.pix = (uint32_t)(I.gy * W + I.px);
   I.sample = k * P.chunk;
   I.s_end = I.sample + P.chunk < P.cam.spp ? I.sample + P.chunk : P.cam.spp;
