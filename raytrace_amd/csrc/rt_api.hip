@@ -49,7 +49,7 @@ struct rt_device_scene {
   int device = 0;
   float* nodes = nullptr;
   float* prims = nullptr;
-  int* prim_mat = nullptr;
+  DevMaterial* prim_shade = nullptr;
   float* prim_uv = nullptr;
   DevMaterial* mats = nullptr;
   DevTexture* texs = nullptr;
@@ -101,7 +101,7 @@ int rt_scene_destroy(rt_device_scene* s) {
   (void)hipSetDevice(s->device);
   (void)hipFree(s->nodes);
   (void)hipFree(s->prims);
-  (void)hipFree(s->prim_mat);
+  (void)hipFree(s->prim_shade);
   (void)hipFree(s->prim_uv);
   (void)hipFree(s->mats);
   (void)hipFree(s->texs);
@@ -132,7 +132,7 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
   s->device = device;
   std::vector<int> status(4, 0);
   if ((rc = upload(&s->nodes, H.nodes)) || (rc = upload(&s->prims, H.prims)) ||
-      (rc = upload(&s->prim_mat, H.prim_mat)) || (rc = upload(&s->prim_uv, H.prim_uv)) ||
+      (rc = upload(&s->prim_shade, H.prim_shade)) || (rc = upload(&s->prim_uv, H.prim_uv)) ||
       (rc = upload(&s->mats, H.mats)) || (rc = upload(&s->texs, H.texs)) || (rc = upload(&s->motions, H.motions)) ||
       (rc = upload(&s->uvframes, H.uvframes)) || (rc = upload(&s->flat_prim, H.flat_prim)) ||
       (rc = upload(&s->texels, H.texels)) || (rc = upload(&s->perlin_perm, H.perlin_perm)) ||
@@ -186,7 +186,7 @@ int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint
   if (rc) return fail(rc, "%s", err.c_str());
   P.nodes = s->nodes;
   P.prims = s->prims;
-  P.prim_mat = s->prim_mat;
+  P.prim_shade = s->prim_shade;
   P.prim_uv = s->prim_uv;
   P.mats = s->mats;
   P.texs = s->texs;

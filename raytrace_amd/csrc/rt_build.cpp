@@ -288,10 +288,17 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   }
   S.mats.assign(sc->n_materials, DevMaterial{});
   for (int i = 0; i < sc->n_materials; ++i) {
-    S.mats[i].kind = sc->materials[i].kind;
-    S.mats[i].tex = sc->materials[i].texture;
-    S.mats[i].param = (float)sc->materials[i].param;
+    DevMaterial& d = S.mats[i];
+    d.kind = sc->materials[i].kind;
+    d.tex = sc->materials[i].texture;
+    d.param = (float)sc->materials[i].param;
+    const rt_texture& t = sc->textures[d.tex];
+    d.tex_const = t.kind == RT_TEX_CONSTANT ? 1 : 0;
+    for (int a = 0; a < 3; ++a) d.c0[a] = (float)t.c0[a];
   }
+  S.prim_shade.assign(S.prim_mat.size(), DevMaterial{});
+  for (size_t j = 0; j < S.prim_mat.size(); ++j)
+    if (S.prim_mat[j] >= 0) S.prim_shade[j] = S.mats[S.prim_mat[j]];
   S.texs.assign(sc->n_textures, DevTexture{});
   for (int i = 0; i < sc->n_textures; ++i) {
     const rt_texture& t = sc->textures[i];

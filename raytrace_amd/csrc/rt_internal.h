@@ -14,7 +14,7 @@
 //                       [3] = (wb.xyz, motion)   with a = (p-q).wa, b = (p-q).wb (Geometry.hs:130-131)
 //               sphere: [0] = (c.xyz, kindflags) [1] = (radius, radius^2, uvframe, gid)
 //                       [2] = (-, -, -, order)   [3] = (-, -, -, motion)
-//   prim_mat: int per primitive (material index, or -1 for medium boundaries)
+//   prim_shade: DevMaterial per primitive (its material, constant textures folded in)
 //   prim_uv : 6 floats per primitive (plane shapes' uv0/uv1/uv2)
 #pragma once
 #include <stdint.h>
@@ -53,11 +53,16 @@ int rt_host_variant(bool flat, int n_media, bool noise);
 #define RT_EV_SCATTER 2u
 #define RT_EV_MEDIA 3u
 
+// Material record (32 B).  A constant texture's colour is folded in (tex_const = 1), so the
+// common case needs no texture-table read; prim_shade holds one copy per primitive, so a surface
+// hit reaches its material in one load (not primitive -> material index -> material -> texture).
 struct DevMaterial {
   int kind;
   int tex;
   float param;
-  int pad;
+  int tex_const;
+  float c0[3];
+  float pad;
 };
 
 struct DevTexture {
@@ -127,7 +132,7 @@ struct FastDiv {
 struct KernelParams {
   const float* nodes;      // 16 floats per node
   const float* prims;      // 16 floats per primitive
-  const int* prim_mat;
+  const DevMaterial* prim_shade;  // per primitive: its material record (DevMaterial)
   const float* prim_uv;    // 6 floats per primitive
   const DevMaterial* mats;
   const DevTexture* texs;
@@ -169,7 +174,8 @@ struct KernelParams {
 struct HostScene {
   std::vector<float> nodes, prims, prim_uv, motions, uvframes, texels, perlin_grad;
   std::vector<int> perlin_perm;
-  std::vector<int> prim_mat;
+  std::vector<int> prim_mat;        // material index per primitive (-1: medium boundary)
+  std::vector<DevMaterial> prim_shade;
   std::vector<int> flat_prim;  // flat scenes: slot -> primitive index
   std::vector<DevMaterial> mats;
   std::vector<DevTexture> texs;

@@ -325,7 +325,6 @@ struct HitInfo {
   f3 p, n;
   bool front;
   float u, v;
-  int mat;
   int gid;
 };
 
@@ -350,7 +349,6 @@ RT_FN HitInfo surface_info(const KernelParams& P, cfp prims, int pi, const RayCt
   int kf = RT_F2I(a.w);
   h.p = R.o + t * R.d;
   h.gid = RT_F2I(b.w);
-  h.mat = ldci(P.prim_mat, pi);
   if ((kf & RT_KIND_MASK) == 0) {
     f3 c = xyz(a);
     if (kf & RT_FLAG_MOTION) c = c + motion_shift(P, RT_F2I(pr[15]), R.time);
@@ -719,17 +717,21 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
     h.front = true;
     h.u = 0.f;
     h.v = 0.f;
-    h.mat = P.media[hit_medium].material;
     h.gid = -1;
   } else {
     h = surface_info(P, prims, best, R, tbest);
   }
-  const RT_CAS DevMaterial* Mp = (const RT_CAS DevMaterial*)P.mats + h.mat;
-  const DevMaterial Mt = DevMaterial{Mp->kind, Mp->tex, Mp->param, 0};
+  // the material: one record load (DevMaterial, per primitive for surfaces)
+  const RT_CAS DevMaterial* Mp = hit_medium >= 0
+                                     ? (const RT_CAS DevMaterial*)P.mats + P.media[hit_medium].material
+                                     : (const RT_CAS DevMaterial*)P.prim_shade + best;
+  const DevMaterial Mt = DevMaterial{Mp->kind, Mp->tex, Mp->param, Mp->tex_const, {0.f, 0.f, 0.f}, 0.f};
   // the material's texture, evaluated once (every material but pitchBlack and dielectric reads
-  // it; one inlined copy of the texture code keeps the register allocation down)
-  f3 tex = mk3(0.f, 0.f, 0.f);
-  if (Mt.kind != RT_MAT_PITCH_BLACK && Mt.kind != RT_MAT_DIELECTRIC) tex = eval_texture<kNoise>(P, Mt.tex, h.u, h.v, h.p);
+  // it; one inlined copy of the texture code keeps the register allocation down); constant
+  // textures come with the record
+  f3 tex = f3{Mp->c0[0], Mp->c0[1], Mp->c0[2]};
+  if (!Mt.tex_const && Mt.kind != RT_MAT_PITCH_BLACK && Mt.kind != RT_MAT_DIELECTRIC)
+    tex = eval_texture<kNoise>(P, Mt.tex, h.u, h.v, h.p);
   u4 w = philox(pix, (uint32_t)sample, (uint32_t)seg, RT_EV_SCATTER, P.key0, P.key1);
   const bool last = seg + 1 >= P.cam.max_depth;  // rayColor (depth - 1) with depth - 1 <= 0 is zero
   f3 newdir = R.d;

@@ -87,7 +87,7 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
   if (rc) return rc;
   P.nodes = H.nodes.data();
   P.prims = H.prims.data();
-  P.prim_mat = H.prim_mat.data();
+  P.prim_shade = H.prim_shade.data();
   P.prim_uv = H.prim_uv.data();
   P.mats = H.mats.data();
   P.texs = H.texs.data();
