@@ -153,7 +153,7 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
   if ((s->variant & RT_VAR_BASE) != RT_VAR_FLAT) {
     // stage as many top (breadth-first) surface nodes as fit beside the stacks in the per-
     // workgroup budget; env RT_AMD_LDS_NODES caps it (0 disables, for experiments)
-    const int room = (RT_LDS_WG_BUDGET - s->stack_depth * RT_BLOCK * (int)sizeof(int)) / 64;
+    const int room = (RT_LDS_WG_BUDGET - s->stack_depth * RT_BLOCK_BVH * (int)sizeof(int)) / 64;
     s->lds_nodes = std::max(0, std::min(H.surface_nodes, room));
     if (const char* e = std::getenv("RT_AMD_LDS_NODES")) s->lds_nodes = std::min(s->lds_nodes, std::max(0, atoi(e)));
   }
@@ -205,7 +205,7 @@ int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint
   P.stack_depth = s->stack_depth;
   P.lds_nodes = s->lds_nodes;
   P.n_prims = s->n_prims;
-  rt_host_plan_work(P, (long long)s->resident_blocks * RT_BLOCK);
+  rt_host_plan_work(P, (long long)s->resident_blocks * rt_block_of(s->variant));
   HIP_TRY(hipSetDevice(s->device));
   // stream-ordered workspace: fixed-point sums, NaN flags, queue counter (graph-capturable)
   const size_t tile_pixels = (size_t)P.tile_rows * P.cam.width;

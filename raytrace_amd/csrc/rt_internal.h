@@ -22,7 +22,10 @@
 #include <string>
 #include <vector>
 
-#define RT_BLOCK 256
+#define RT_BLOCK 256          // flat kernel workgroup
+#ifndef RT_BLOCK_BVH
+#define RT_BLOCK_BVH 256      // BVH kernel workgroup (its lanes share one LDS copy of the top nodes)
+#endif
 #define RT_STACK_DEPTH 32
 #define RT_MAX_MEDIA 8
 #define RT_MAX_TARGETS 8
@@ -32,7 +35,9 @@
 #define RT_LEAF_SHIFT 6       // leaf encoding ~(first << 6 | count - 1), count <= 64
 #define RT_FLAT_MAX 32        // a set of at most this many leaves is one flat leaf (no traversal)
 #define RT_LDS_PRIMS_MAX 256  // flat kernel: scenes of at most this many primitives
+#ifndef RT_LDS_WG_BUDGET
 #define RT_LDS_WG_BUDGET 30720  // BVH kernel LDS per workgroup (stack + staged nodes): 5 per CU
+#endif
 #define RT_EMPTY_ROOT ((int)0x80000000)
 
 // render-kernel variants (rt_kernel.hip)
@@ -41,6 +46,8 @@
 #define RT_VAR_BVH 2           // BVH, traversal decoupled from shading (default for BVH scenes)
 #define RT_VAR_BASE 3
 #define RT_VAR_NOISE 4         // flag: the scene has noise / marble textures (their code compiled in)
+// workgroup size of a variant's render kernel
+inline int rt_block_of(int variant) { return (variant & RT_VAR_BASE) == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH; }
 // host choice of variant (rt_build.cpp); env RT_AMD_VARIANT overrides the base for experiments
 int rt_host_variant(bool flat, int n_media, bool noise);
 

@@ -89,7 +89,7 @@ struct AtomicCommit {
 #define RT_WAVES_BVH 5
 #endif
 template <int kVar, bool kNoise>
-__global__ __launch_bounds__(RT_BLOCK)
+__global__ __launch_bounds__(kVar == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH)
 __attribute__((amdgpu_waves_per_eu(kVar == RT_VAR_FLAT ? (kNoise ? RT_WAVES_FLAT_NOISE : RT_WAVES_FLAT)
                                                          : RT_WAVES_BVH)))
 void rt_render_kernel(KernelParams P) {
@@ -101,14 +101,14 @@ void rt_render_kernel(KernelParams P) {
     overflow = rtk::lane_loop_lockstep<true, kNoise>(P, grab, commit, rtk::Trav{nullptr, 0, nullptr}, P.prims);
   } else {
     // LDS: [stack_depth][RT_BLOCK] stack words, then the top P.lds_nodes BVH nodes (64 B each)
-    rtk::v4* lds_nodes = reinterpret_cast<rtk::v4*>(smem + P.stack_depth * RT_BLOCK);
+    rtk::v4* lds_nodes = reinterpret_cast<rtk::v4*>(smem + P.stack_depth * RT_BLOCK_BVH);
     const float4* src = reinterpret_cast<const float4*>(P.nodes);
-    for (int i = threadIdx.x; i < 4 * P.lds_nodes; i += RT_BLOCK) {
+    for (int i = threadIdx.x; i < 4 * P.lds_nodes; i += RT_BLOCK_BVH) {
       const float4 q = src[i];
       lds_nodes[i] = rtk::v4{q.x, q.y, q.z, q.w};
     }
     __syncthreads();
-    const rtk::Trav W{smem + threadIdx.x, RT_BLOCK, lds_nodes};
+    const rtk::Trav W{smem + threadIdx.x, RT_BLOCK_BVH, lds_nodes};
     if constexpr (kVar == RT_VAR_BVH_LOCKSTEP)
       overflow = rtk::lane_loop_lockstep<false, kNoise>(P, grab, commit, W, P.prims);
     else
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void rt_encode8_kernel(const float* __restrict
 
 static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
   return (variant & RT_VAR_BASE) == RT_VAR_FLAT ? 0
-                                                 : (size_t)stack_depth * RT_BLOCK * sizeof(int) + (size_t)lds_nodes * 64;
+                                                 : (size_t)stack_depth * RT_BLOCK_BVH * sizeof(int) + (size_t)lds_nodes * 64;
 }
 
 // the kernel instantiation of a variant code (base variant | RT_VAR_NOISE)
@@ -186,7 +186,10 @@ static render_fn render_kernel_of(int variant) {
 int rt_render_resident_blocks(int device, int stack_depth, int variant, int lds_nodes) {
   int per_cu = 0, cus = 0;
   size_t lds = render_lds_bytes(stack_depth, variant, lds_nodes);
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_kernel_of(variant), RT_BLOCK, lds);
+  if (lds > 65536 && hipFuncSetAttribute((const void*)render_kernel_of(variant),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return -1;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_kernel_of(variant), rt_block_of(variant), lds);
   if (e != hipSuccess) return -1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return -1;
   if (per_cu < 1) per_cu = 1;
@@ -195,10 +198,11 @@ int rt_render_resident_blocks(int device, int stack_depth, int variant, int lds_
 
 int rt_launch_render(const KernelParams& p, int grid_blocks, int variant, void* stream) {
   if (p.n_items <= 0 || grid_blocks <= 0) return 0;
-  long long need = ((long long)p.n_items + RT_BLOCK - 1) / RT_BLOCK;
+  const int block = rt_block_of(variant);
+  long long need = ((long long)p.n_items + block - 1) / block;
   int grid = need < grid_blocks ? (int)need : grid_blocks;
   size_t lds = render_lds_bytes(p.stack_depth, variant, p.lds_nodes);
-  hipLaunchKernelGGL(render_kernel_of(variant), dim3(grid), dim3(RT_BLOCK), lds, (hipStream_t)stream, p);
+  hipLaunchKernelGGL(render_kernel_of(variant), dim3(grid), dim3(block), lds, (hipStream_t)stream, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -142,3 +142,18 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
   return RT_OK;
 }
 }
+
+extern "C" {
+// scene summary of the host build (test tooling): n_nodes, surface_nodes, max_depth, n_prims, flat
+int rt_emu_scene_info(const rt_scene* sc, int* info) {
+  HostScene H;
+  int rc = rt_host_build_scene(sc, H, g_err);
+  if (rc) return rc;
+  info[0] = H.n_nodes;
+  info[1] = H.surface_nodes;
+  info[2] = H.max_depth;
+  info[3] = H.n_prims;
+  info[4] = H.flat ? 1 : 0;
+  return RT_OK;
+}
+}
