@@ -8,7 +8,9 @@ One step = one full frame of the config (Cornell box 600x600, 200 spp, depth 50,
 target, seed 234 — test/Main.hs:188-218) with the scene already resident in HBM.  With N
 ranks (one process per GPU) the frame's rows are dealt to ranks in blocks of 4
 (rt_exec row interleave) and the framebuffer tiles are gathered over RCCL (all_gather into one
-tensor) inside the timed step; `value` = pixels x spp of all ranks / max-over-ranks time.
+tensor) inside the timed region — asynchronously, so frame i+1 renders while frame i's gather is in
+flight (two frame buffers); the clock stops after every frame is rendered AND gathered.
+`value` = pixels x spp of all ranks / max-over-ranks time.
 
 Extra fields: `roofline` (the render kernel's SURVEY.md §8(d) algorithmic bytes per launch /
 its HIP-event-timed duration vs the 8 TB/s HBM peak; `traffic` = PMC-measured HBM bytes per
@@ -140,13 +142,24 @@ def main():
     h, w, spp = image_height(cs), cs.cs_imageWidth, cs.cs_samplesPerPixel
     scene = DeviceScene(world, device=local_rank)
     rows = shard_rows(h, n, args.row_block)
-    tile = torch.empty((rows, w, 3), dtype=torch.float32, device=dev)
-    gathered = torch.empty((n * rows, w, 3), dtype=torch.float32, device=dev) if n > 1 else None
+    # two frame buffers: frame i+1 renders while the RCCL gather of frame i is in flight on the
+    # collective's own stream (the compute stream waits for gather i-1 before reusing its tile)
+    nbuf = 2 if n > 1 else 1
+    tiles = [torch.empty((rows, w, 3), dtype=torch.float32, device=dev) for _ in range(nbuf)]
+    gathered = [torch.empty((n * rows, w, 3), dtype=torch.float32, device=dev) for _ in range(nbuf)] if n > 1 else None
+    works = [None] * nbuf
     stream = torch.cuda.current_stream(dev)
 
     ev = []
+    frame = [0]
 
     def step(timed):
+        b = frame[0] % nbuf
+        frame[0] += 1
+        tile = tiles[b]
+        if works[b] is not None:
+            works[b].wait()  # stream-ordered: the gather that read this tile has completed
+            works[b] = None
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
@@ -157,22 +170,29 @@ def main():
             ev.append((e0, e1))
         if n > 1:
             if args.dist_backend == "nccl":
-                dist.all_gather_into_tensor(gathered, tile)
+                works[b] = dist.all_gather_into_tensor(gathered[b], tile, async_op=True)
             else:  # rehearsal path: through host memory
                 parts = [torch.empty((rows, w, 3), dtype=torch.float32) for _ in range(n)]
                 dist.all_gather(parts, tile.cpu())
-                gathered.copy_(torch.cat(parts).to(dev))
+                gathered[b].copy_(torch.cat(parts).to(dev))
+
+    def drain():
+        for k in range(nbuf):
+            if works[k] is not None:
+                works[k].wait()
+                works[k] = None
+        torch.cuda.synchronize(dev)
 
     for _ in range(args.warmup):
         step(False)
-    torch.cuda.synchronize(dev)
+    drain()
     if n > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
-    torch.cuda.synchronize(dev)
+    drain()  # every frame rendered AND gathered
     if n > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -186,11 +206,12 @@ def main():
     check = None
     if args.check or rank == 0:
         import numpy as np
+        last = (frame[0] - 1) % nbuf
         if n > 1:
-            tiles = gathered.view(n, rows, w, 3).cpu().numpy()
-            img = assemble_shards(tiles, h, args.row_block)
+            parts = gathered[last].view(n, rows, w, 3).cpu().numpy()
+            img = assemble_shards(parts, h, args.row_block)
         else:
-            img = tile[:h].cpu().numpy()
+            img = tiles[last][:h].cpu().numpy()
         check = {"finite": bool(np.isfinite(img).all()), "mean_rgb": [round(float(x), 5) for x in img.reshape(-1, 3).mean(0)]}
 
     total_samples = h * w * spp

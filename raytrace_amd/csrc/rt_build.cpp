@@ -197,9 +197,63 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   if (const char* e = std::getenv("RT_AMD_NO_ALIAS"))  // experiments: always traverse boundaries
     if (atoi(e)) std::fill(alias.begin(), alias.end(), 0);
 
-  // one BVH per set; primitives stored in leaf order, set after set
-  std::vector<int> order;
+  // Large-primitive prefix of the surface set (BVH scenes).  Primitives whose box is a large
+  // fraction of the whole set's (the Cornell walls around a mesh, demo1's ground sphere) overlap
+  // almost every ray and sit at the top of any BVH; taken out of it, they are tested first by
+  // the whole wave with wave-uniform records (scalar loads, like the flat kernel), and their
+  // closest hit then bounds the traversal of the remaining BVH (rt_trace.h prefix_hits).  The
+  // 64-bit closest-hit key carries each leaf's global depth-first order, so the result is the
+  // same closest hit, tie for tie.  Only static primitives; grouped by class like a flat set.
+  std::vector<int> prefix;  // caller indices, class-grouped
+  int prefix_cnt[3] = {0, 0, 0};
+  {
+    bool want = (int)sets[0].size() > RT_FLAT_MAX + RT_PREFIX_MAX;
+    if (const char* e = std::getenv("RT_AMD_NO_PREFIX"))  // experiments: everything in the BVH
+      if (atoi(e)) want = false;
+    if (want) {
+      auto area = [](const double* lo, const double* hi) {
+        double d[3];
+        for (int a = 0; a < 3; ++a) d[a] = std::max(0.0, hi[a] - lo[a]);
+        return 2.0 * (d[0] * d[1] + d[1] * d[2] + d[2] * d[0]);
+      };
+      double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+      for (const BuildPrim& b : sets[0])
+        for (int a = 0; a < 3; ++a) {
+          lo[a] = std::min(lo[a], b.lo[a]);
+          hi[a] = std::max(hi[a], b.hi[a]);
+        }
+      const double root_area = area(lo, hi);
+      std::vector<std::pair<double, int>> big;  // (area, position in sets[0])
+      for (size_t j = 0; j < sets[0].size(); ++j) {
+        const BuildPrim& b = sets[0][j];
+        const double a = area(b.lo, b.hi);
+        if (sc->prims[b.index].motion < 0 && a >= RT_PREFIX_AREA * root_area) big.push_back({-a, (int)j});
+      }
+      std::stable_sort(big.begin(), big.end());
+      if (big.size() > RT_PREFIX_MAX) big.resize(RT_PREFIX_MAX);
+      std::vector<char> taken(sets[0].size(), 0);
+      for (auto& b : big) taken[b.second] = 1;
+      auto cls = [&](int i) {
+        const int k = sc->prims[i].kind;
+        return k == RT_PRIM_PARALLELOGRAM ? 0 : k == RT_PRIM_TRIANGLE ? 1 : 2;
+      };
+      std::vector<BuildPrim> rest;
+      for (size_t j = 0; j < sets[0].size(); ++j) {
+        if (taken[j])
+          prefix.push_back(sets[0][j].index);
+        else
+          rest.push_back(sets[0][j]);
+      }
+      std::stable_sort(prefix.begin(), prefix.end(), [&](int x, int y) { return cls(x) < cls(y); });
+      for (int i : prefix) prefix_cnt[cls(i)]++;
+      sets[0].swap(rest);
+    }
+  }
+
+  // one BVH per set; primitives stored in leaf order, set after set (the prefix first)
+  std::vector<int> order(prefix);
   std::vector<int> roots(n_sets), set_begin(n_sets + 1, 0);
+  set_begin[0] = (int)prefix.size();
   S.nodes.clear();
   S.max_depth = 0;
   for (int s = 0; s < n_sets; ++s) {
@@ -215,7 +269,15 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   if (S.max_depth > RT_STACK_DEPTH)
     return fail(err, RT_E_STACK, "BVH depth %d exceeds the traversal stack (%d)", S.max_depth, RT_STACK_DEPTH);
   const int n = (int)order.size();
-  S.flat = S.nodes.empty() && n <= RT_LDS_PRIMS_MAX;
+  S.flat = S.nodes.empty() && n <= RT_LDS_PRIMS_MAX && prefix.empty();
+  if (!prefix.empty()) {  // BVH scenes: flat_sets[0] describes the surface prefix
+    DevFlatSet& F = S.flat_sets[0];
+    F.first = 0;
+    F.end_quad = prefix_cnt[0];
+    F.end_tri = F.end_quad + prefix_cnt[1];
+    F.end_sphere = F.end_tri + prefix_cnt[2];
+    F.end = F.end_sphere;
+  }
   if (S.flat) {
     // group each set's single leaf by class (rt_internal.h DevFlatSet); stable within a class
     auto cls = [&](int i) {

@@ -35,6 +35,10 @@
 #define RT_LEAF_SHIFT 6       // leaf encoding ~(first << 6 | count - 1), count <= 64
 #define RT_FLAT_MAX 32        // a set of at most this many leaves is one flat leaf (no traversal)
 #define RT_LDS_PRIMS_MAX 256  // flat kernel: scenes of at most this many primitives
+#define RT_PREFIX_MAX 16      // BVH scenes: at most this many large surface primitives tested first
+#ifndef RT_PREFIX_AREA
+#define RT_PREFIX_AREA 0.1    // ... those whose box area is >= this fraction of the surface set's box
+#endif
 #ifndef RT_LDS_WG_BUDGET
 #define RT_LDS_WG_BUDGET 30720  // BVH kernel LDS per workgroup (stack + staged nodes): 5 per CU
 #endif

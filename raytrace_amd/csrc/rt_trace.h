@@ -301,8 +301,8 @@ RT_FN void test_rec(const KernelParams& P, const PrimRec& r, int pi, const RayCt
 }
 
 // A static primitive of a known kind (flat sets are grouped by class: rt_build.cpp).
-template <int kKind>
-RT_FN void test_static(const PrimRec& r, const RayCtx& R, float tmin, float tmin_up, Closest& C) {
+template <int kKind, bool kKeyOnly = true>
+RT_FN void test_static(const PrimRec& r, const RayCtx& R, float tmin, float tmin_up, Closest& C, int pi = 0) {
   RT_COUNT(1);
   const bool self = RT_F2I(r.b.w) == R.self_gid;
   float t, q;
@@ -310,7 +310,22 @@ RT_FN void test_static(const PrimRec& r, const RayCtx& R, float tmin, float tmin
     isect_sphere(r, R.o, R, tmin, tmin_up, self, t, q);
   else
     isect_plane<kKind == RT_PRIM_CLASS_QUAD ? 1 : 0>(r, R.o, R, tmin_up, self, t, q);
-  consider<true>(C, t, q, RT_F2I(r.c.w), 0);
+  consider<kKeyOnly>(C, t, q, RT_F2I(r.c.w), pi);
+}
+
+// BVH scenes: the surface set's large-primitive prefix (rt_build.cpp; P.flat_sets[0]), tested
+// before the traversal so that its closest hit bounds it.  The range is a kernel argument, so
+// the records are wave-uniform (scalar loads) even when only some lanes start a query here.
+RT_FN void prefix_hits(const KernelParams& P, cfp prims, const RayCtx& R, float tmin, Closest& C) {
+  const DevFlatSet& S = P.flat_sets[0];
+  if (S.end == S.first) return;
+  const float tmin_up = float_up(tmin);
+  int k = S.first;
+  const RT_CAS PrimRec64* rp = (const RT_CAS PrimRec64*)prims + k;
+  for (; k < S.end_quad; ++k, ++rp) test_static<RT_PRIM_CLASS_QUAD, false>(ld_rec64(rp), R, tmin, tmin_up, C, k);
+  for (; k < S.end_tri; ++k, ++rp) test_static<RT_PRIM_CLASS_TRI, false>(ld_rec64(rp), R, tmin, tmin_up, C, k);
+  for (; k < S.end_sphere; ++k, ++rp)
+    test_static<RT_PRIM_CLASS_SPHERE, false>(ld_rec64(rp), R, tmin, tmin_up, C, k);
 }
 
 
@@ -637,10 +652,9 @@ RT_FN_SPEC void closest<true>(const KernelParams& P, cfp prims, int root, int se
 template <>
 RT_FN_SPEC void closest<false>(const KernelParams& P, cfp prims, int root, int set, const RayCtx& R, float tmin,
                           Closest& C, const Trav& W, int* overflow) {
-  (void)prims;
-  (void)set;
   TravState S;
   trav_begin(S, root, tmin);
+  if (set == 0) prefix_hits(P, prims, R, tmin, S.C);
   while (!trav_done(S)) trav_round(P, R, S, W, *overflow);
   C = S.C;
 }
@@ -1001,6 +1015,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
       hit_medium = -1;
       tbest = kInf;
       trav_begin(S, P.surface_root, kTmin);
+      prefix_hits(P, prims, R, kTmin, S.C);
       state = ST_TRACE;
     }
     // ---- traversal rounds; a finished query starts the segment's next one in place

@@ -119,6 +119,16 @@ def test_kernel_variants_bitwise_identical(gpu, monkeypatch, name):
         assert np.array_equal(img, imgs[0], equal_nan=True)
 
 
+@pytest.mark.parametrize("name", ["bunny_cornell", "demo1"])
+def test_large_primitive_prefix_is_exact(gpu, monkeypatch, name):
+    fn = {"bunny_cornell": scenes.bunny_cornell, "demo1": scenes.demo1}[name]
+    cs, world, seed = fn(width=96, spp=8)
+    a = R.raytrace(cs, world, seed)
+    monkeypatch.setenv("RT_AMD_NO_PREFIX", "1")
+    b = R.raytrace(cs, world, seed)
+    assert np.array_equal(a, b, equal_nan=True)
+
+
 def test_medium_boundary_alias_is_exact(gpu, monkeypatch):
     cs, world, seed = scenes.pawn_fog(width=96, spp=8)
     a = R.raytrace(cs, world, seed)

@@ -156,6 +156,22 @@ def test_medium_boundary_alias_is_exact(emu_mod, monkeypatch, variant):
     assert np.array_equal(a, b, equal_nan=True)
 
 
+@pytest.mark.parametrize("variant", ["1", "2"])
+@pytest.mark.parametrize("name", ["bunny_cornell", "demo1"])
+def test_large_primitive_prefix_is_exact(emu_mod, monkeypatch, variant, name):
+    """The surface set's large primitives (Cornell walls, demo1's ground sphere) tested before the
+    BVH instead of inside it: the closest-hit key carries the global depth-first order, so the
+    image is bit-identical, and the traversal does less work."""
+    fn = {"bunny_cornell": scenes.bunny_cornell, "demo1": scenes.demo1}[name]
+    cs, world, seed = fn(width=48, spp=4)
+    monkeypatch.setenv("RT_AMD_VARIANT", variant)
+    a, ca = emu_mod.render(cs, world, seed, counters=True)
+    monkeypatch.setenv("RT_AMD_NO_PREFIX", "1")
+    b, cb = emu_mod.render(cs, world, seed, counters=True)
+    assert np.array_equal(a, b, equal_nan=True)
+    assert ca["bvh_nodes"] < cb["bvh_nodes"]
+
+
 def test_perlin_tables(oracle_mod):
     """The product's Perlin tables: three permutations of 0..255 (Noise.hs:60-92) and the 256
     gradients of Noise.hs:94-98, identical to the oracle's independent C restatement."""
