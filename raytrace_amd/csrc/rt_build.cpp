@@ -62,6 +62,122 @@ int fail(std::string& err, int code, const char* fmt, ...) {
   return code;
 }
 
+
+// Box groups (rt_internal.h DevBox): parallelograms that are full faces of one rectangular box.
+struct BoxFound {
+  d3 c, a[3];       // corner, axis_k / L_k
+  int face[6];      // caller primitive index of face f = 2 axis + side, -1 if absent
+};
+
+// Among `rects` (caller indices of static parallelograms of one set) find boxes with >= 3 faces;
+// every primitive is used at most once.  Binary64, relative tolerance 1e-9 of the box size.
+std::vector<BoxFound> find_boxes(const rt_scene* sc, const std::vector<int>& rects) {
+  std::vector<BoxFound> out;
+  const int n = (int)rects.size();
+  std::vector<char> used(n, 0);
+  auto corners = [&](int i, d3* c4) {
+    const double* p = sc->prims[rects[i]].p;
+    d3 q = D3(p), u = D3(p + 3), v = D3(p + 6);
+    c4[0] = q;
+    c4[1] = q + u;
+    c4[2] = q + v;
+    c4[3] = q + u + v;
+  };
+  auto is_rect = [&](int i) {
+    const double* p = sc->prims[rects[i]].p;
+    d3 u = D3(p + 3), v = D3(p + 6);
+    double lu = std::sqrt(dot(u, u)), lv = std::sqrt(dot(v, v));
+    return lu > 0 && lv > 0 && std::fabs(dot(u, v)) <= 1e-12 * lu * lv;
+  };
+  for (int i = 0; i < n; ++i) {
+    if (used[i] || !is_rect(i)) continue;
+    const double* pi = sc->prims[rects[i]].p;
+    d3 ui = D3(pi + 3), vi = D3(pi + 6);
+    d3 e0 = divs(ui, std::sqrt(dot(ui, ui))), e1 = divs(vi, std::sqrt(dot(vi, vi))), e2 = cross(e0, e1);
+    e2 = divs(e2, std::sqrt(dot(e2, e2)));
+    d3 ci[4];
+    corners(i, ci);
+    for (int j = 0; j < n; ++j) {
+      if (j == i || used[j] || !is_rect(j)) continue;
+      d3 cj[4];
+      corners(j, cj);
+      const double h = dot(e2, cj[0] - ci[0]);
+      const double size = std::sqrt(std::max(dot(ui, ui), dot(vi, vi)));
+      const double tol = 1e-9 * std::max(size, std::fabs(h));
+      if (!(std::fabs(h) > tol)) continue;
+      bool match = true;  // j = i translated by h e2, corner for corner (as sets)
+      for (int a = 0; a < 4 && match; ++a) {
+        d3 t = cj[a] - smul(h, e2);
+        bool any = false;
+        for (int b = 0; b < 4; ++b) {
+          d3 d = t - ci[b];
+          any = any || std::sqrt(dot(d, d)) <= tol;
+        }
+        match = any;
+      }
+      if (!match) continue;
+      // the box spanned by i and j, in the frame (e0, e1, e2)
+      const d3 E[3] = {e0, e1, e2};
+      double lo[3], hi[3];
+      for (int k = 0; k < 3; ++k) {
+        lo[k] = INFINITY;
+        hi[k] = -INFINITY;
+        for (int a = 0; a < 4; ++a) {
+          for (const d3& p : {ci[a], cj[a]}) {
+            double x = dot(E[k], p - ci[0]);
+            lo[k] = std::min(lo[k], x);
+            hi[k] = std::max(hi[k], x);
+          }
+        }
+      }
+      BoxFound B;
+      B.c = ci[0] + smul(lo[0], e0) + smul(lo[1], e1) + smul(lo[2], e2);
+      for (int k = 0; k < 3; ++k) B.a[k] = divs(E[k], hi[k] - lo[k]);
+      for (int f = 0; f < 6; ++f) B.face[f] = -1;
+      std::vector<int> members;
+      for (int m = 0; m < n; ++m) {
+        if (used[m] || !is_rect(m)) continue;
+        d3 cm[4];
+        corners(m, cm);
+        double sc4[4][3];
+        for (int a = 0; a < 4; ++a)
+          for (int k = 0; k < 3; ++k) sc4[a][k] = dot(B.a[k], cm[a] - B.c);
+        const double et = 1e-9;
+        auto near01 = [&](double x, int& bit) {
+          if (std::fabs(x) <= et) return bit = 0, true;
+          if (std::fabs(x - 1) <= et) return bit = 1, true;
+          return false;
+        };
+        int face = -1;
+        for (int ax = 0; ax < 3 && face < 0; ++ax) {
+          int side0 = -1, mask = 0;
+          bool ok = true;
+          for (int a = 0; a < 4 && ok; ++a) {
+            int bits[3];
+            for (int k = 0; k < 3 && ok; ++k) ok = near01(sc4[a][k], bits[k]);
+            if (!ok) break;
+            if (side0 < 0) side0 = bits[ax];
+            ok = bits[ax] == side0;
+            const int b1 = bits[(ax + 1) % 3], b2 = bits[(ax + 2) % 3];
+            mask |= 1 << (b1 * 2 + b2);
+          }
+          if (ok && mask == 15) face = 2 * ax + side0;  // the four corners of that face
+        }
+        if (face >= 0 && B.face[face] < 0) {
+          B.face[face] = rects[m];
+          members.push_back(m);
+        }
+      }
+      if (members.size() >= 3) {
+        for (int m : members) used[m] = 1;
+        out.push_back(B);
+        break;
+      }
+    }
+  }
+  return out;
+}
+
 }  // namespace
 
 int rt_host_image_height(const rt_camera_settings* cs) {
@@ -297,7 +413,66 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
       F.end_tri = F.end_quad + cnt[1];
       F.end_sphere = F.end_tri + cnt[2];
       F.end = F.end_sphere + cnt[3];
-      F.pad[0] = F.pad[1] = F.pad[2] = 0;
+      F.box_first = F.box_end = 0;
+      F.pad = 0;
+    }
+  }
+  // box groups among each flat set's static parallelograms (and the surface prefix): their
+  // faces move to the end of the set's range, after the tested classes (DevBox)
+  std::vector<BoxFound> boxes;
+  std::vector<int> box_face_pos;  // per box: position in `order` of its first face
+  {
+    bool want = true;
+    if (const char* e = std::getenv("RT_AMD_NO_BOX"))  // experiments: every face its own test
+      if (atoi(e)) want = false;
+    for (int s = 0; s < n_sets && want; ++s) {
+      if (!S.flat && !(s == 0 && !prefix.empty())) break;
+      DevFlatSet& F = S.flat_sets[s];
+      const int set_end = S.flat ? set_begin[s + 1] : (int)prefix.size();
+      std::vector<int> quads(order.begin() + F.first, order.begin() + F.end_quad);
+      std::vector<BoxFound> found;
+      for (const BoxFound& B : find_boxes(sc, quads)) {
+        // the faces' key orders and gids must fit the 5-bit offset codes (slot spans are at
+        // most the order spans)
+        int olo = INT32_MAX, ohi = INT32_MIN, glo = INT32_MAX, ghi = INT32_MIN;
+        for (int f = 0; f < 6; ++f) {
+          if (B.face[f] < 0) continue;
+          const rt_prim& p = sc->prims[B.face[f]];
+          olo = std::min(olo, p.order);
+          ohi = std::max(ohi, p.order);
+          glo = std::min(glo, p.gid);
+          ghi = std::max(ghi, p.gid);
+        }
+        if ((long long)ohi - olo < RT_BOX_NO_FACE && (long long)ghi - glo < RT_BOX_NO_FACE) found.push_back(B);
+      }
+      F.box_first = F.box_end = (int)boxes.size();
+      if (found.empty()) continue;
+      std::vector<char> in_box(sc->n_prims, 0);
+      for (const BoxFound& B : found)
+        for (int f = 0; f < 6; ++f)
+          if (B.face[f] >= 0) in_box[B.face[f]] = 1;
+      std::vector<int> rest, faces;
+      int removed = 0;
+      for (int j = F.first; j < set_end; ++j) {
+        if (in_box[order[j]]) {
+          ++removed;
+          continue;
+        }
+        rest.push_back(order[j]);
+      }
+      for (const BoxFound& B : found) {
+        box_face_pos.push_back(F.first + (int)rest.size() + (int)faces.size());
+        for (int f = 0; f < 6; ++f)
+          if (B.face[f] >= 0) faces.push_back(B.face[f]);
+        boxes.push_back(B);
+      }
+      std::copy(rest.begin(), rest.end(), order.begin() + F.first);
+      std::copy(faces.begin(), faces.end(), order.begin() + F.first + rest.size());
+      F.end_quad -= removed;
+      F.end_tri -= removed;
+      F.end_sphere -= removed;
+      F.end -= removed;
+      F.box_end = (int)boxes.size();
     }
   }
   // flat scenes: slot of each primitive (rank of its order within the set) and slot -> index
@@ -313,6 +488,50 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
         slot_of[pos[r]] = set_begin[s] + (int)r;
         S.flat_prim[set_begin[s] + r] = pos[r];
       }
+    }
+  }
+  {
+    std::vector<int> pos_of(sc->n_prims, -1);
+    for (int j = 0; j < n; ++j) pos_of[order[j]] = j;
+    S.boxes.clear();
+    for (size_t b = 0; b < boxes.size(); ++b) {
+      const BoxFound& B = boxes[b];
+      DevBox d;
+      std::memset(&d, 0, sizeof d);
+      put3(d.c, B.c);
+      put3(d.a0, B.a[0]);
+      put3(d.a1, B.a[1]);
+      put3(d.a2, B.a[2]);
+      int ord[6], gid[6], prm[6];
+      int ob = INT32_MAX, gb = INT32_MAX, pb = INT32_MAX;
+      for (int f = 0; f < 6; ++f) {
+        if (B.face[f] < 0) continue;
+        const int j = pos_of[B.face[f]];
+        ord[f] = S.flat ? slot_of[j] : sc->prims[B.face[f]].order;
+        gid[f] = sc->prims[B.face[f]].gid;
+        prm[f] = j;
+        ob = std::min(ob, ord[f]);
+        gb = std::min(gb, gid[f]);
+        pb = std::min(pb, prm[f]);
+      }
+      d.ord_base = ob;
+      d.gid_base = gb;
+      d.prim_base = pb;
+      bool fits = true;
+      for (int f = 0; f < 6; ++f) {
+        int oo = RT_BOX_NO_FACE, go = RT_BOX_NO_FACE, po = RT_BOX_NO_FACE;
+        if (B.face[f] >= 0) {
+          oo = ord[f] - ob;
+          go = gid[f] - gb;
+          po = prm[f] - pb;
+          fits = fits && oo < RT_BOX_NO_FACE && go < RT_BOX_NO_FACE && po < RT_BOX_NO_FACE;
+        }
+        d.ord_code |= oo << (5 * f);
+        d.gid_code |= go << (5 * f);
+        d.prim_code |= po << (5 * f);
+      }
+      if (!fits) return fail(err, RT_E_GENERIC, "box group %d: face offsets exceed the 5-bit codes", (int)b);
+      S.boxes.push_back(d);
     }
   }
   S.prims.assign((size_t)n * 16, 0.0f);

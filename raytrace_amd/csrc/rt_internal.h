@@ -109,7 +109,32 @@ struct DevMedium {
 #define RT_PRIM_CLASS_SPHERE 0
 struct DevFlatSet {
   int first, end_quad, end_tri, end_sphere, end;
-  int pad[3];
+  int box_first, box_end;  // its box groups: KernelParams::boxes[box_first, box_end)
+  int pad;
+};
+
+// Box groups.  Parallelograms of one flat set (or of the BVH scenes' surface prefix) that are
+// full faces of one rectangular box — `cuboid` (Geometry.hs:154-166) under a rigid transform, or
+// the walls of the Cornell box — are tested together: the ray meets the box's surface at most
+// twice (entry and exit, Kay-Kajiya slabs in the box frame), so one slab test plus a table
+// lookup of the face replaces one parallelogram test per face.  Faces are numbered
+// f = 2 * axis + side (side 1 = the s_axis = 1 end); each face's key order, gid and primitive
+// are base + a 5-bit offset packed at bit 5 f of the codes (31: the box has no such face).
+// The face primitives stay in the primitive array (shading reads them) after the set's tested
+// range.  The closest hit is the reference's up to FP32 rounding at the boxes' edges.
+#define RT_BOX_NO_FACE 31
+struct DevBox {
+  float c[3];      // corner (s = 0 on every axis)
+  int ord_base;    // key order (flat: slot; prefix: depth-first order) of the faces
+  float a0[3];     // axis_0 / L_0: s_0 = a0 . (p - c) in [0, 1] inside
+  int ord_code;
+  float a1[3];
+  int gid_base;
+  float a2[3];
+  int gid_code;
+  int prim_base;   // primitive index of the faces
+  int prim_code;
+  int pad[2];
 };
 
 struct DevTarget {
@@ -153,6 +178,7 @@ struct KernelParams {
   const int* perlin_perm;  // 3 x 256 permutation entries (Noise.hs permX / permY / permZ)
   const float* perlin_grad;  // 256 gradients, 4 floats each (xyz, -)
   const int* flat_prim;    // flat scenes: closest-hit slot -> primitive index (DevFlatSet)
+  const DevBox* boxes;     // box groups of the flat sets / the surface prefix (DevBox)
   float* out;
   int* status;             // device word: nonzero on stack overflow
   // persistent-lane work queue (rt_trace.h lane_loop): items = n_chunks x tile pixels
@@ -167,6 +193,7 @@ struct KernelParams {
   int trav_exit_pct;          // BVH kernel: leave traversal when <= this % of live lanes trace
   int n_prims;                // all leaves (every set), staged in LDS by the flat kernel
   int surface_root;
+  int surface_prefix;         // BVH scenes: flat_sets[0] is the surface set's prefix (rt_trace.h prefix_hits)
   int n_media;
   int n_targets;
   float rem_prob;
@@ -188,6 +215,7 @@ struct HostScene {
   std::vector<int> prim_mat;        // material index per primitive (-1: medium boundary)
   std::vector<DevMaterial> prim_shade;
   std::vector<int> flat_prim;  // flat scenes: slot -> primitive index
+  std::vector<DevBox> boxes;   // box groups (DevBox)
   std::vector<DevMaterial> mats;
   std::vector<DevTexture> texs;
   int surface_root = RT_EMPTY_ROOT;

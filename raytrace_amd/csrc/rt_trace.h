@@ -313,13 +313,59 @@ RT_FN void test_static(const PrimRec& r, const RayCtx& R, float tmin, float tmin
   consider<kKeyOnly>(C, t, q, RT_F2I(r.c.w), pi);
 }
 
+// A box group (rt_internal.h DevBox): slabs in the box frame give the entry and exit points of
+// the ray on the box surface; each is a candidate hit on the face it lies on (if the box has
+// that face), with the same validity rules as a parallelogram test (t > tmin, not the face the
+// ray leaves).  Wave-uniform record (scalar loads).
+RT_FN int box_field(int base, int code, int f, bool& present) {
+  const int off = (int)((unsigned)code >> (5 * f)) & 31;
+  present = off != RT_BOX_NO_FACE;
+  return base + off;
+}
+template <bool kKeyOnly>
+RT_FN void box_candidate(const RT_CAS DevBox* B, int f, float t, float q, const RayCtx& R, Closest& C) {
+  bool present;
+  const int ord = box_field(B->ord_base, B->ord_code, f, present);
+  const int gid = box_field(B->gid_base, B->gid_code, f, present);
+  int prim = 0;
+  if constexpr (!kKeyOnly) prim = box_field(B->prim_base, B->prim_code, f, present);
+  consider<kKeyOnly>(C, t, present && gid != R.self_gid ? q : -1.0f, ord, prim);
+}
+template <bool kKeyOnly>
+RT_FN void test_box(const RT_CAS DevBox* B, const RayCtx& R, float tmin_up, Closest& C) {
+  RT_COUNT(1);
+  const f3 oc = R.o - f3{B->c[0], B->c[1], B->c[2]};
+  const f3 ax[3] = {f3{B->a0[0], B->a0[1], B->a0[2]}, f3{B->a1[0], B->a1[1], B->a1[2]},
+                    f3{B->a2[0], B->a2[1], B->a2[2]}};
+  float lo[3], hi[3];
+  int flip[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float inv = RT_RCP(dot(ax[k], R.d));
+    const float s = dot(ax[k], oc);
+    const float t0 = -s * inv, t1 = fmaf(-s, inv, inv);  // the s = 0 and s = 1 planes
+    flip[k] = t1 < t0 ? 1 : 0;                            // entering through the s = 1 end
+    lo[k] = fminf(t0, t1);
+    hi[k] = fmaxf(t0, t1);
+  }
+  const float tn = fmaxf(fmaxf(lo[0], lo[1]), lo[2]), tf = fminf(fminf(hi[0], hi[1]), hi[2]);
+  const int an = lo[0] == tn ? 0 : lo[1] == tn ? 1 : 2;
+  const int af = hi[0] == tf ? 0 : hi[1] == tf ? 1 : 2;
+  const int fn = 2 * an + (an == 0 ? flip[0] : an == 1 ? flip[1] : flip[2]);
+  const int ff = 2 * af + 1 - (af == 0 ? flip[0] : af == 1 ? flip[1] : flip[2]);
+  const float gap = tf - tn;  // >= 0: the line meets the box
+  box_candidate<kKeyOnly>(B, fn, tn, fminf(gap, tn - tmin_up), R, C);
+  box_candidate<kKeyOnly>(B, ff, tf, fminf(gap, tf - tmin_up), R, C);
+}
+
 // BVH scenes: the surface set's large-primitive prefix (rt_build.cpp; P.flat_sets[0]), tested
 // before the traversal so that its closest hit bounds it.  The range is a kernel argument, so
 // the records are wave-uniform (scalar loads) even when only some lanes start a query here.
 RT_FN void prefix_hits(const KernelParams& P, cfp prims, const RayCtx& R, float tmin, Closest& C) {
   const DevFlatSet& S = P.flat_sets[0];
-  if (S.end == S.first) return;
+  if (!P.surface_prefix || (S.end == S.first && S.box_end == S.box_first)) return;
   const float tmin_up = float_up(tmin);
+  for (int b = S.box_first; b < S.box_end; ++b) test_box<false>((const RT_CAS DevBox*)P.boxes + b, R, tmin_up, C);
   int k = S.first;
   const RT_CAS PrimRec64* rp = (const RT_CAS PrimRec64*)prims + k;
   for (; k < S.end_quad; ++k, ++rp) test_static<RT_PRIM_CLASS_QUAD, false>(ld_rec64(rp), R, tmin, tmin_up, C, k);
@@ -631,6 +677,7 @@ RT_FN_SPEC void closest<true>(const KernelParams& P, cfp prims, int root, int se
 #else
     const float tmin_up = float_up(tmin);
 #endif
+    for (int b = S.box_first; b < S.box_end; ++b) test_box<true>((const RT_CAS DevBox*)P.boxes + b, R, tmin_up, C);
     int k = S.first;
     const RT_CAS PrimRec64* rp = (const RT_CAS PrimRec64*)prims + k;  // one 64-B scalar load per record
     for (; k < S.end_quad; ++k, ++rp) test_static<RT_PRIM_CLASS_QUAD>(ld_rec64(rp), R, tmin, tmin_up, C);

@@ -16,7 +16,7 @@ import os
 from .camera import constBackground, defaultCameraSettings, grayFade, sky
 from .core import V3, degrees, mkStdGen, midpoint, norm, sub
 from .geometry import (boundingBox, bvhTree, cuboid, constantMedium, group, parallelogram, pureGeometry, readObj,
-                       rotateY, scale, sphere, transform, transformVertices, translate, triangleMesh)
+                       rotateX, rotateY, scale, sphere, transform, transformVertices, translate, triangleMesh)
 from .material import (checkerTexture, constantTexture, dielectric, isotropic, lambertian, lightSource,
                        marbleTexture, metal, mirror, noiseTexture)
 from .core import fromCorners
@@ -183,6 +183,24 @@ def noise_test(width=400, spp=100, depth=50, seed=7):
     return settings, world, mkStdGen(seed)
 
 
+def box_gallery(width=200, spp=16, depth=50):
+    """Test scene for box groups (DevBox): the Cornell walls around a glass cuboid at an oblique
+    orientation (rays inside it exit through a face), a fuzzy-metal cuboid under a reflecting
+    transform (det -1) and a mirror cuboid.  Not a reference scene."""
+    import numpy as np
+    walls, white = cornell_walls()
+    reflect_x = np.diag([-1.0, 1.0, 1.0, 1.0])
+    world = group(walls + [
+        transform(translate(V3(300, 120, 300)) @ rotateY(degrees(30)) @ rotateX(degrees(25)),
+                  dielectric(1.5) << cuboid(fromCorners(V3(-60, -60, -60), V3(60, 60, 60)))),
+        transform(translate(V3(420, 0, 120)) @ reflect_x @ rotateY(degrees(-20)),
+                  metal(0.2, constantTexture(V3(0.8, 0.85, 0.9))) << cuboid(fromCorners(V3(0, 0, 0), V3(90, 200, 90)))),
+        transform(translate(V3(90, 0, 380)) @ rotateY(degrees(40)),
+                  mirror(constantTexture(V3(0.9, 0.9, 0.9))) << cuboid(fromCorners(V3(0, 0, 0), V3(120, 120, 120)))),
+    ])
+    return cornell_settings(width, spp, depth, redirect=True), world, mkStdGen(77)
+
+
 CONFIGS = {
     "readme": readme_scene,
     "cornell": cornell_box,
@@ -191,4 +209,5 @@ CONFIGS = {
     "pawn_fog": pawn_fog,
     "pawn_test": pawn_test,
     "noise_test": noise_test,
+    "box_gallery": box_gallery,
 }

@@ -97,8 +97,10 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
   P.perlin_perm = H.perlin_perm.data();
   P.perlin_grad = H.perlin_grad.data();
   P.flat_prim = H.flat_prim.data();
+  P.boxes = H.boxes.data();
   P.out = out;
   P.surface_root = H.surface_root;
+  P.surface_prefix = H.flat ? 0 : 1;
   P.n_media = H.n_media;
   for (int k = 0; k < H.n_media; ++k) P.media[k] = H.media[k];
   for (int k = 0; k <= RT_MAX_MEDIA; ++k) P.flat_sets[k] = H.flat_sets[k];

@@ -112,6 +112,9 @@ def test_kernel_variants_bitwise_identical(gpu, monkeypatch, name):
           "demo1": scenes.demo1}[name]
     cs, world, seed = fn(width=96, spp=8)
     imgs = []
+    # the flat kernel tests cuboid faces as box groups, the BVH kernels run on a flat scene test
+    # them one by one (same result up to rounding at the box edges): compare with box groups off
+    monkeypatch.setenv("RT_AMD_NO_BOX", "1")
     for v in ("0", "1", "2"):
         monkeypatch.setenv("RT_AMD_VARIANT", v)
         imgs.append(R.raytrace(cs, world, seed))
@@ -123,10 +126,24 @@ def test_kernel_variants_bitwise_identical(gpu, monkeypatch, name):
 def test_large_primitive_prefix_is_exact(gpu, monkeypatch, name):
     fn = {"bunny_cornell": scenes.bunny_cornell, "demo1": scenes.demo1}[name]
     cs, world, seed = fn(width=96, spp=8)
+    monkeypatch.setenv("RT_AMD_NO_BOX", "1")  # exact claim: per-face tests in and out of the BVH
     a = R.raytrace(cs, world, seed)
     monkeypatch.setenv("RT_AMD_NO_PREFIX", "1")
     b = R.raytrace(cs, world, seed)
     assert np.array_equal(a, b, equal_nan=True)
+
+
+@pytest.mark.parametrize("name", ["cornell", "box_gallery"])
+def test_box_groups_match_oracle(gpu, oracle_mod, monkeypatch, name):
+    fn = {"cornell": scenes.cornell_box, "box_gallery": scenes.box_gallery}[name]
+    cs, world, seed = fn(width=96, spp=8)
+    a = R.raytrace(cs, world, seed)
+    ref = oracle_mod.render(cs, world, seed, mode=oracle_mod.RNG_PHILOX)
+    assert np.isfinite(a).all()
+    assert pixel_agreement(a, ref) >= 0.99
+    monkeypatch.setenv("RT_AMD_NO_BOX", "1")
+    b = R.raytrace(cs, world, seed)
+    assert pixel_agreement(a, b) >= 0.995
 
 
 def test_medium_boundary_alias_is_exact(gpu, monkeypatch):

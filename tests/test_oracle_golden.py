@@ -137,6 +137,9 @@ def test_kernel_variants_render_bitwise_identical_images(emu_mod, monkeypatch, n
     fn = {"cornell": scenes.cornell_box, "pawn_fog": scenes.pawn_fog, "bunny_cornell": scenes.bunny_cornell}[name]
     cs, world, seed = fn(width=48, spp=4)
     imgs = []
+    # the flat kernel tests cuboid faces as box groups, the BVH kernels run on a flat scene test
+    # them one by one (same result up to rounding at the box edges): compare with box groups off
+    monkeypatch.setenv("RT_AMD_NO_BOX", "1")
     for v in ("0", "1", "2"):
         monkeypatch.setenv("RT_AMD_VARIANT", v)
         imgs.append(emu_mod.render(cs, world, seed))
@@ -165,11 +168,31 @@ def test_large_primitive_prefix_is_exact(emu_mod, monkeypatch, variant, name):
     fn = {"bunny_cornell": scenes.bunny_cornell, "demo1": scenes.demo1}[name]
     cs, world, seed = fn(width=48, spp=4)
     monkeypatch.setenv("RT_AMD_VARIANT", variant)
+    monkeypatch.setenv("RT_AMD_NO_BOX", "1")  # exact claim: per-face tests in and out of the BVH
     a, ca = emu_mod.render(cs, world, seed, counters=True)
     monkeypatch.setenv("RT_AMD_NO_PREFIX", "1")
     b, cb = emu_mod.render(cs, world, seed, counters=True)
     assert np.array_equal(a, b, equal_nan=True)
     assert ca["bvh_nodes"] < cb["bvh_nodes"]
+
+
+@pytest.mark.parametrize("name", ["cornell", "box_gallery", "bunny_cornell"])
+def test_box_groups_match_per_face_tests(oracle_mod, emu_mod, monkeypatch, name):
+    """Cuboid faces and the Cornell walls tested as box groups (one slab test per box, DevBox)
+    render the image of one parallelogram test per face up to FP32 rounding at the box edges,
+    and match the FP64 oracle (which walks the reference's group of parallelograms) per pixel.
+    box_gallery has rays inside a glass cuboid (exit faces) and a reflected (det -1) cuboid."""
+    fn = {"cornell": scenes.cornell_box, "box_gallery": scenes.box_gallery, "bunny_cornell": scenes.bunny_cornell}[name]
+    cs, world, seed = fn(width=64, spp=8)
+    a, ca = emu_mod.render(cs, world, seed, counters=True)
+    monkeypatch.setenv("RT_AMD_NO_BOX", "1")
+    b, cb = emu_mod.render(cs, world, seed, counters=True)
+    assert ca["prims_tested"] < cb["prims_tested"]
+    assert np.isfinite(a).all()
+    assert pixel_agreement(a, b) >= 0.995
+    ref = oracle_mod.render(cs, world, seed, mode=oracle_mod.RNG_PHILOX)
+    assert pixel_agreement(a, ref) >= 0.995
+    np.testing.assert_allclose(a.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=5e-3)
 
 
 def test_perlin_tables(oracle_mod):
