@@ -58,7 +58,7 @@ struct rt_device_scene {
   float* texels = nullptr;
   int* perlin_perm = nullptr;
   float* perlin_grad = nullptr;
-  int* flat_prim = nullptr;
+  float* flat_recs = nullptr;
   DevBox* boxes = nullptr;
   int* status = nullptr;
   int surface_root = RT_EMPTY_ROOT;
@@ -111,7 +111,7 @@ int rt_scene_destroy(rt_device_scene* s) {
   (void)hipFree(s->texels);
   (void)hipFree(s->perlin_perm);
   (void)hipFree(s->perlin_grad);
-  (void)hipFree(s->flat_prim);
+  (void)hipFree(s->flat_recs);
   (void)hipFree(s->boxes);
   (void)hipFree(s->status);
   delete s;
@@ -136,7 +136,7 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
   if ((rc = upload(&s->nodes, H.nodes)) || (rc = upload(&s->prims, H.prims)) ||
       (rc = upload(&s->prim_shade, H.prim_shade)) || (rc = upload(&s->prim_uv, H.prim_uv)) ||
       (rc = upload(&s->mats, H.mats)) || (rc = upload(&s->texs, H.texs)) || (rc = upload(&s->motions, H.motions)) ||
-      (rc = upload(&s->uvframes, H.uvframes)) || (rc = upload(&s->flat_prim, H.flat_prim)) || (rc = upload(&s->boxes, H.boxes)) ||
+      (rc = upload(&s->uvframes, H.uvframes)) || (rc = upload(&s->flat_recs, H.flat_recs)) || (rc = upload(&s->boxes, H.boxes)) ||
       (rc = upload(&s->texels, H.texels)) || (rc = upload(&s->perlin_perm, H.perlin_perm)) ||
       (rc = upload(&s->perlin_grad, H.perlin_grad)) ||
       (rc = upload(&s->status, status))) {
@@ -197,7 +197,7 @@ int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint
   P.texels = s->texels;
   P.perlin_perm = s->perlin_perm;
   P.perlin_grad = s->perlin_grad;
-  P.flat_prim = s->flat_prim;
+  P.flat_recs = s->flat_recs;
   P.boxes = s->boxes;
   P.status = s->status;
   P.out = d_out_rgb;

@@ -478,7 +478,6 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   // flat scenes: slot of each primitive (rank of its order within the set) and slot -> index
   std::vector<int> slot_of(n, 0);
   if (S.flat) {
-    S.flat_prim.assign(n, 0);
     for (int s = 0; s < n_sets; ++s) {
       std::vector<int> pos;
       for (int j = set_begin[s]; j < set_begin[s + 1]; ++j) pos.push_back(j);
@@ -486,7 +485,6 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
                        [&](int x, int y) { return sc->prims[order[x]].order < sc->prims[order[y]].order; });
       for (size_t r = 0; r < pos.size(); ++r) {
         slot_of[pos[r]] = set_begin[s] + (int)r;
-        S.flat_prim[set_begin[s] + r] = pos[r];
       }
     }
   }
@@ -509,7 +507,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
         const int j = pos_of[B.face[f]];
         ord[f] = S.flat ? slot_of[j] : sc->prims[B.face[f]].order;
         gid[f] = sc->prims[B.face[f]].gid;
-        prm[f] = j;
+        prm[f] = S.flat ? slot_of[j] : j;
         ob = std::min(ob, ord[f]);
         gb = std::min(gb, gid[f]);
         pb = std::min(pb, prm[f]);
@@ -566,6 +564,21 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     f[11] = ibits(S.flat ? slot_of[j] : p.order);
     f[15] = ibits(p.motion);
     S.prim_mat[j] = p.set == 0 ? p.material : -1;
+  }
+  S.flat_recs.clear();
+  if (S.flat) {  // test order -> slot order for the shading arrays (prim index = slot)
+    S.flat_recs = S.prims;
+    std::vector<float> prims(S.prims.size()), uv(S.prim_uv.size());
+    std::vector<int> mat(S.prim_mat.size());
+    for (int j = 0; j < n; ++j) {
+      const int k = slot_of[j];
+      std::copy(S.flat_recs.begin() + 16 * (size_t)j, S.flat_recs.begin() + 16 * (size_t)(j + 1), prims.begin() + 16 * (size_t)k);
+      std::copy(S.prim_uv.begin() + 6 * (size_t)j, S.prim_uv.begin() + 6 * (size_t)(j + 1), uv.begin() + 6 * (size_t)k);
+      mat[k] = S.prim_mat[j];
+    }
+    S.prims.swap(prims);
+    S.prim_uv.swap(uv);
+    S.prim_mat.swap(mat);
   }
   S.mats.assign(sc->n_materials, DevMaterial{});
   for (int i = 0; i < sc->n_materials; ++i) {

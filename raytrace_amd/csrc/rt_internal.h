@@ -103,7 +103,8 @@ struct DevMedium {
 // [end_sphere, end) moving primitives of any kind.  Each record's order word holds its SLOT:
 // set first + rank of its depth-first `order` within the set, so the 64-bit closest-hit key
 // (t, slot) keeps the reference's tie-break whatever the test order, and the winner's index is
-// one lookup, flat_prim[slot], after the loop (the loop itself only tracks the key).
+// its slot: flat scenes store `prims` in slot order and test class-grouped copies (flat_recs), so
+// the loop tracks only the key and the winner's primitive index IS its slot.
 #define RT_PRIM_CLASS_QUAD 1
 #define RT_PRIM_CLASS_TRI 2
 #define RT_PRIM_CLASS_SPHERE 0
@@ -177,7 +178,7 @@ struct KernelParams {
   const float* texels;     // image textures: 4 floats per texel (linear RGB, -)
   const int* perlin_perm;  // 3 x 256 permutation entries (Noise.hs permX / permY / permZ)
   const float* perlin_grad;  // 256 gradients, 4 floats each (xyz, -)
-  const int* flat_prim;    // flat scenes: closest-hit slot -> primitive index (DevFlatSet)
+  const float* flat_recs;  // flat scenes: the test records, class-grouped (DevFlatSet ranges)
   const DevBox* boxes;     // box groups of the flat sets / the surface prefix (DevBox)
   float* out;
   int* status;             // device word: nonzero on stack overflow
@@ -214,7 +215,7 @@ struct HostScene {
   std::vector<int> perlin_perm;
   std::vector<int> prim_mat;        // material index per primitive (-1: medium boundary)
   std::vector<DevMaterial> prim_shade;
-  std::vector<int> flat_prim;  // flat scenes: slot -> primitive index
+  std::vector<float> flat_recs;  // flat scenes: class-grouped copies of the records (prims is in slot order)
   std::vector<DevBox> boxes;   // box groups (DevBox)
   std::vector<DevMaterial> mats;
   std::vector<DevTexture> texs;

@@ -403,7 +403,9 @@ RT_FN bool prim_front(const KernelParams& P, cfp prims, int pi, const RayCtx& R,
   return dot(xyz(a), R.d) < 0.0f;
 }
 
-RT_FN HitInfo surface_info(const KernelParams& P, cfp prims, int pi, const RayCtx& R, float t) {
+// need_uv: the material reads a (u, v) texture; otherwise the texture coordinates (sphereUV's
+// atan2 / acos, the triangle's uv lerp and its prim_uv loads) are skipped.
+RT_FN HitInfo surface_info(const KernelParams& P, cfp prims, int pi, const RayCtx& R, float t, bool need_uv) {
   HitInfo h;
   cfp pr = prims + 16 * (size_t)pi;
   v4 a = ldc4(pr), b = ldc4(pr + 4);
@@ -416,6 +418,8 @@ RT_FN HitInfo surface_info(const KernelParams& P, cfp prims, int pi, const RayCt
     f3 outward = RT_RCP(b.x) * (h.p - c);
     h.front = dot(R.d, outward) <= 0.0f;
     h.n = h.front ? outward : -outward;
+    h.u = h.v = 0.0f;
+    if (!need_uv) return h;
     int uvf = RT_F2I(b.z);
     f3 on = outward;
     if (uvf >= 0) {
@@ -430,6 +434,8 @@ RT_FN HitInfo surface_info(const KernelParams& P, cfp prims, int pi, const RayCt
     float denom = dot(n, R.d);
     h.front = denom < 0.0f;
     h.n = h.front ? n : -n;
+    h.u = h.v = 0.0f;
+    if (!need_uv) return h;
     f3 o = R.o;
     if (kf & RT_FLAG_MOTION) o = o - motion_shift(P, RT_F2I(pr[15]), R.time);
     f3 prel = (o + t * R.d) - xyz(b);
@@ -665,6 +671,7 @@ RT_FN void trav_round(const KernelParams& P, const RayCtx& R, TravState& S, cons
 template <>
 RT_FN_SPEC void closest<true>(const KernelParams& P, cfp prims, int root, int set, const RayCtx& R, float tmin, Closest& C,
                          const Trav& W, int* overflow) {
+  (void)prims;
   (void)root;
   (void)W;
   (void)overflow;
@@ -679,7 +686,7 @@ RT_FN_SPEC void closest<true>(const KernelParams& P, cfp prims, int root, int se
 #endif
     for (int b = S.box_first; b < S.box_end; ++b) test_box<true>((const RT_CAS DevBox*)P.boxes + b, R, tmin_up, C);
     int k = S.first;
-    const RT_CAS PrimRec64* rp = (const RT_CAS PrimRec64*)prims + k;  // one 64-B scalar load per record
+    const RT_CAS PrimRec64* rp = (const RT_CAS PrimRec64*)P.flat_recs + k;  // one 64-B scalar load per record
     for (; k < S.end_quad; ++k, ++rp) test_static<RT_PRIM_CLASS_QUAD>(ld_rec64(rp), R, tmin, tmin_up, C);
     for (; k < S.end_tri; ++k, ++rp) test_static<RT_PRIM_CLASS_TRI>(ld_rec64(rp), R, tmin, tmin_up, C);
     for (; k < S.end_sphere; ++k, ++rp) test_static<RT_PRIM_CLASS_SPHERE>(ld_rec64(rp), R, tmin, tmin_up, C);
@@ -690,7 +697,7 @@ RT_FN_SPEC void closest<true>(const KernelParams& P, cfp prims, int root, int se
     const uint32_t hi = (uint32_t)(C.key >> 32);
     if (hi < 0x7f800000u) {  // a finite t won
       C.t = __builtin_bit_cast(float, hi);
-      C.prim = ldci(P.flat_prim, (int)(uint32_t)C.key);
+      C.prim = (int)(uint32_t)C.key;  // slot = primitive index (flat scenes store prims in slot order)
     }
   }
 }
@@ -771,6 +778,14 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
     return true;
   }
   bool terminate = false;
+  // the material: one record load (DevMaterial, per primitive for surfaces)
+  const RT_CAS DevMaterial* Mp = hit_medium >= 0
+                                     ? (const RT_CAS DevMaterial*)P.mats + P.media[hit_medium].material
+                                     : (const RT_CAS DevMaterial*)P.prim_shade + best;
+  const DevMaterial Mt = DevMaterial{Mp->kind, Mp->tex, Mp->param, Mp->tex_const, {0.f, 0.f, 0.f}, 0.f};
+  // every material but pitchBlack and dielectric reads its texture; constant textures come with
+  // the record, the others are evaluated once (one inlined copy keeps the register allocation down)
+  const bool need_tex = !Mt.tex_const && Mt.kind != RT_MAT_PITCH_BLACK && Mt.kind != RT_MAT_DIELECTRIC;
   HitInfo h;
   if (hit_medium >= 0) {
     h.p = R.o + tbest * R.d;
@@ -780,19 +795,10 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
     h.v = 0.f;
     h.gid = -1;
   } else {
-    h = surface_info(P, prims, best, R, tbest);
+    h = surface_info(P, prims, best, R, tbest, need_tex);
   }
-  // the material: one record load (DevMaterial, per primitive for surfaces)
-  const RT_CAS DevMaterial* Mp = hit_medium >= 0
-                                     ? (const RT_CAS DevMaterial*)P.mats + P.media[hit_medium].material
-                                     : (const RT_CAS DevMaterial*)P.prim_shade + best;
-  const DevMaterial Mt = DevMaterial{Mp->kind, Mp->tex, Mp->param, Mp->tex_const, {0.f, 0.f, 0.f}, 0.f};
-  // the material's texture, evaluated once (every material but pitchBlack and dielectric reads
-  // it; one inlined copy of the texture code keeps the register allocation down); constant
-  // textures come with the record
   f3 tex = f3{Mp->c0[0], Mp->c0[1], Mp->c0[2]};
-  if (!Mt.tex_const && Mt.kind != RT_MAT_PITCH_BLACK && Mt.kind != RT_MAT_DIELECTRIC)
-    tex = eval_texture<kNoise>(P, Mt.tex, h.u, h.v, h.p);
+  if (need_tex) tex = eval_texture<kNoise>(P, Mt.tex, h.u, h.v, h.p);
   u4 w = philox(pix, (uint32_t)sample, (uint32_t)seg, RT_EV_SCATTER, P.key0, P.key1);
   const bool last = seg + 1 >= P.cam.max_depth;  // rayColor (depth - 1) with depth - 1 <= 0 is zero
   f3 newdir = R.d;

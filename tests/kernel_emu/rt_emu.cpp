@@ -96,7 +96,7 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
   P.texels = H.texels.data();
   P.perlin_perm = H.perlin_perm.data();
   P.perlin_grad = H.perlin_grad.data();
-  P.flat_prim = H.flat_prim.data();
+  P.flat_recs = H.flat_recs.data();
   P.boxes = H.boxes.data();
   P.out = out;
   P.surface_root = H.surface_root;
