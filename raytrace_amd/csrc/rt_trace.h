@@ -716,7 +716,11 @@ RT_FN_SPEC void closest<false>(const KernelParams& P, cfp prims, int root, int s
 // ------------------------------------------------------------------ per-path pieces
 // Ray.hs:157-172, 229: pixel jitter, time, defocus-disk point -> primary ray
 RT_FN void camera_ray(const KernelParams& P, uint32_t pix, int sample, int px, int gy, RayCtx& R) {
+#ifdef RT_EXP_CHEAP_CAMERA  // ablation (wrong image): measures the camera block's Philox cost
+  u4 w0 = u4{pix * 0x9E3779B9u + (uint32_t)sample, pix ^ ((uint32_t)sample * 0x85EBCA6Bu), 0u, 0u};
+#else
   u4 w0 = philox(pix, (uint32_t)sample, 0u, RT_EV_CAMERA0, P.key0, P.key1);
+#endif
   R.time = u01(w0.z);
   f3 origin = ld3(P.cam.center);
   if (P.cam.disk_u[0] != 0.0f || P.cam.disk_u[1] != 0.0f || P.cam.disk_u[2] != 0.0f || P.cam.disk_v[0] != 0.0f ||
