@@ -12,8 +12,15 @@ tensor) inside the timed region — asynchronously, so frame i+1 renders while f
 flight (two frame buffers); the clock stops after every frame is rendered AND gathered.
 `value` = pixels x spp of all ranks / max-over-ranks time.
 
+Frames of flat scenes (the Cornell box) alternate between two HIP streams (--streams 2, the
+default for them): a frame's last long paths occupy few CUs, and the next frame's persistent
+workgroups fill the rest instead of waiting (Cornell +4 % at 1 GPU, +26 % on one rank's share of
+an 8-GPU frame).
+
 Extra fields: `roofline` (the render kernel's SURVEY.md §8(d) algorithmic bytes per launch /
-its HIP-event-timed duration vs the 8 TB/s HBM peak; `traffic` = PMC-measured HBM bytes per
+its device time per frame, from HIP events over the timed region — `kernel_ms`, the span of the
+timed frames / frames; `launch_ms` is the average single-launch duration, longer because two
+launches overlap — vs the 8 TB/s HBM peak; `traffic` = PMC-measured HBM bytes per
 launch from the committed rocprofv3 summary, when present), `issue_roofline` (the kernel's
 PMC-counted VALU wave-instructions per launch / its time vs the chip's VALU issue ceiling — the
 physical limiter of this cache-resident, branchy FP32 kernel) and `cpu_baseline`
@@ -109,6 +116,12 @@ def main():
     ap.add_argument("--row-block", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="gather + assemble + sanity-check the frame after timing")
+    ap.add_argument("--streams", type=int, default=0, choices=[0, 1, 2],
+                    help="frames alternate between this many HIP streams (2: frame i+1 fills the CUs that "
+                         "frame i's last long paths leave idle); 0 = auto: 2 for flat scenes, 1 for BVH "
+                         "scenes (two LDS-staging BVH launches interfere: bunny 20.7 -> 22.4 ms per frame)")
+    ap.add_argument("--sim-shards", type=int, default=1,
+                    help="diagnostic, one process: render only shard 0 of N (one rank's share of an N-GPU frame)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, the real path); gloo gathers through host memory (N>1 rehearsal on one "
                          "GPU, with RT_BENCH_ONE_DEVICE=1 mapping every rank to device 0)")
@@ -119,7 +132,7 @@ def main():
 
     from raytrace_amd import scenes
     from raytrace_amd.camera import image_height
-    from raytrace_amd.ray import DeviceScene, assemble_shards, shard_rows
+    from raytrace_amd.ray import DeviceScene, assemble_shards, shard_row_index, shard_rows
 
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -127,6 +140,7 @@ def main():
     if world_size != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world_size}; using WORLD_SIZE")
     n = world_size
+    n_sh, sh = (args.sim_shards, 0) if world_size == 1 and args.sim_shards > 1 else (n, rank)
     if os.environ.get("RT_BENCH_ONE_DEVICE") == "1":
         local_rank = 0
     torch.cuda.set_device(local_rank)
@@ -141,21 +155,28 @@ def main():
     cs, world, seed = fn()
     h, w, spp = image_height(cs), cs.cs_imageWidth, cs.cs_samplesPerPixel
     scene = DeviceScene(world, device=local_rank)
-    rows = shard_rows(h, n, args.row_block)
+    rows = shard_rows(h, n_sh, args.row_block)
     # two frame buffers: frame i+1 renders while the RCCL gather of frame i is in flight on the
     # collective's own stream (the compute stream waits for gather i-1 before reusing its tile)
-    nbuf = 2 if n > 1 else 1
+    if args.streams == 0:
+        args.streams = 2 if scene.stats()["bvh_nodes"] == 0 else 1
+    nbuf = 2 if n > 1 or args.streams > 1 else 1
     tiles = [torch.empty((rows, w, 3), dtype=torch.float32, device=dev) for _ in range(nbuf)]
     gathered = [torch.empty((n * rows, w, 3), dtype=torch.float32, device=dev) for _ in range(nbuf)] if n > 1 else None
     works = [None] * nbuf
-    stream = torch.cuda.current_stream(dev)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(args.streams - 1)]
 
     ev = []
     frame = [0]
 
     def step(timed):
         b = frame[0] % nbuf
+        stream = streams[frame[0] % len(streams)]
         frame[0] += 1
+        with torch.cuda.stream(stream):
+            frame_step(b, stream, timed)
+
+    def frame_step(b, stream, timed):
         tile = tiles[b]
         if works[b] is not None:
             works[b].wait()  # stream-ordered: the gather that read this tile has completed
@@ -163,7 +184,7 @@ def main():
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        scene.render_async(cs, seed, tile.data_ptr(), stream.cuda_stream, n_shards=n, shard=rank,
+        scene.render_async(cs, seed, tile.data_ptr(), stream.cuda_stream, n_shards=n_sh, shard=sh,
                            row_block=args.row_block)
         if timed:
             e1.record(stream)
@@ -201,7 +222,14 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
+    # per-launch HIP-event duration, and the device time per frame: the HIP-event span of the timed
+    # frames / frames (with --streams 2 consecutive launches overlap, so a launch lasts longer than
+    # the device time it costs per frame)
+    launch_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
+    kernel_ms = launch_ms
+    if ev:
+        span = max(ev[0][0].elapsed_time(b) for _, b in ev[-len(streams):])
+        kernel_ms = span / len(ev)
 
     check = None
     if args.check or rank == 0:
@@ -211,22 +239,24 @@ def main():
             parts = gathered[last].view(n, rows, w, 3).cpu().numpy()
             img = assemble_shards(parts, h, args.row_block)
         else:
-            img = tiles[last][:h].cpu().numpy()
+            img = tiles[last][:h].cpu().numpy() if n_sh == 1 else tiles[last].cpu().numpy()
         check = {"finite": bool(np.isfinite(img).all()), "mean_rgb": [round(float(x), 5) for x in img.reshape(-1, 3).mean(0)]}
 
     total_samples = h * w * spp
+    if n_sh != n:  # --sim-shards: the samples of the one shard rendered
+        total_samples = int((shard_row_index(h, n_sh, sh, args.row_block) < h).sum()) * w * spp
     value = total_samples * args.steps / elapsed / 1e6
     if rank == 0:
         with open(os.path.join(ROOT, "tests", "golden", "algbytes.json")) as f:
             alg = json.load(f)["configs"][args.config]
         b_sample = alg["bytes_per_sample"]
-        from raytrace_amd.ray import shard_row_index
-        real_rows = int((shard_row_index(h, n, rank, args.row_block) < h).sum())
+        real_rows = int((shard_row_index(h, n_sh, sh, args.row_block) < h).sum())
         samples_per_launch = real_rows * w * spp
         achieved = b_sample * samples_per_launch / (kernel_ms / 1e3) / 1e9
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.config),
                     "kernel": "rt_render_kernel", "kernel_ms": round(kernel_ms, 4),
+                    "launch_ms": round(launch_ms, 4), "concurrent_launches": len(streams),
                     "bytes_per_sample": round(b_sample, 1), "samples_per_launch": samples_per_launch}
         cpu = None
         if n == 1 and not args.no_cpu_baseline:

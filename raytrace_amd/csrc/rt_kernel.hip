@@ -28,6 +28,7 @@ struct WaveGrab {
   int* counter;
   int pool_base;
   int pool_left;
+  int offset;  // ids [0, offset) are the waves' initial pools, handed out without atomics
   __device__ __forceinline__ int operator()(bool need) {
     const unsigned long long m = __ballot(need);
     if (m == 0ull) return 0;
@@ -42,7 +43,7 @@ struct WaveGrab {
     } else {
       int base = 0;
       if (lane == __ffsll((unsigned long long)m) - 1) base = atomicAdd(counter, RT_POOL);
-      base = __builtin_amdgcn_readfirstlane(__shfl(base, __ffsll((unsigned long long)m) - 1));
+      base = __builtin_amdgcn_readfirstlane(__shfl(base, __ffsll((unsigned long long)m) - 1)) + offset;
       item = rank < pool_left ? pool_base + rank : base + (rank - pool_left);
       const int used = cnt - pool_left;
       pool_base = base + used;
@@ -94,7 +95,11 @@ __attribute__((amdgpu_waves_per_eu(kVar == RT_VAR_FLAT ? (kNoise ? RT_WAVES_FLAT
                                                          : RT_WAVES_BVH)))
 void rt_render_kernel(KernelParams P) {
   extern __shared__ int smem[];
-  WaveGrab grab{P.counter, 0, 0};
+  // every wave starts with a static pool (its wave index x RT_POOL): at launch all resident waves
+  // would otherwise queue up on the counter at once (~80 us at ~88 returning atomics per us)
+  const int waves = (int)(gridDim.x * (blockDim.x / 64));
+  const int wave = (int)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
+  WaveGrab grab{P.counter, wave * RT_POOL, RT_POOL, waves * RT_POOL};
   AtomicCommit commit{P.accum, P.nanflag};
   int overflow;
   if constexpr (kVar == RT_VAR_FLAT) {
