@@ -6,7 +6,7 @@
 
 One step = one full frame of the config (Cornell box 600x600, 200 spp, depth 50, redirect
 target, seed 234 — test/Main.hs:188-218) with the scene already resident in HBM.  With N
-ranks (one process per GPU) the frame's rows are dealt to ranks in blocks of 4
+ranks (one process per GPU) the frame's rows are dealt to ranks round-robin (--row-block 1)
 (rt_exec row interleave) and the framebuffer tiles are gathered over RCCL (all_gather into one
 tensor) inside the timed region — asynchronously, so frame i+1 renders while frame i's gather is in
 flight (two frame buffers); the clock stops after every frame is rendered AND gathered.
@@ -113,7 +113,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="cornell", choices=["cornell", "readme", "demo1", "bunny_cornell", "pawn_fog"])
-    ap.add_argument("--row-block", type=int, default=4)
+    ap.add_argument("--row-block", type=int, default=1,
+                    help="rows are dealt to ranks in blocks of this many (1: 600 rows split exactly 8 ways)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="gather + assemble + sanity-check the frame after timing")
     ap.add_argument("--streams", type=int, default=0, choices=[0, 1, 2],
