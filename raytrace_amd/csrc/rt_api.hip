@@ -155,7 +155,7 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
   if ((s->variant & RT_VAR_BASE) != RT_VAR_FLAT) {
     // stage as many top (breadth-first) surface nodes as fit beside the stacks in the per-
     // workgroup budget; env RT_AMD_LDS_NODES caps it (0 disables, for experiments)
-    const int room = (RT_LDS_WG_BUDGET - s->stack_depth * RT_BLOCK_BVH * (int)sizeof(int)) / 64;
+    const int room = (RT_LDS_WG_BUDGET - (s->stack_depth + 1) * RT_BLOCK_BVH * (int)sizeof(int)) / 64;
     s->lds_nodes = std::max(0, std::min(H.surface_nodes, room));
     if (const char* e = std::getenv("RT_AMD_LDS_NODES")) s->lds_nodes = std::min(s->lds_nodes, std::max(0, atoi(e)));
   }

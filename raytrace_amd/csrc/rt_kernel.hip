@@ -105,8 +105,9 @@ void rt_render_kernel(KernelParams P) {
   if constexpr (kVar == RT_VAR_FLAT) {
     overflow = rtk::lane_loop_lockstep<true, kNoise>(P, grab, commit, rtk::Trav{nullptr, 0, nullptr}, P.prims);
   } else {
-    // LDS: [stack_depth][RT_BLOCK] stack words, then the top P.lds_nodes BVH nodes (64 B each)
-    rtk::v4* lds_nodes = reinterpret_cast<rtk::v4*>(smem + P.stack_depth * RT_BLOCK_BVH);
+    // LDS: [stack_depth + 1][RT_BLOCK_BVH] stack words (the last row a spare write target), then
+    // the top P.lds_nodes BVH nodes (64 B each)
+    rtk::v4* lds_nodes = reinterpret_cast<rtk::v4*>(smem + (P.stack_depth + 1) * RT_BLOCK_BVH);
     const float4* src = reinterpret_cast<const float4*>(P.nodes);
     for (int i = threadIdx.x; i < 4 * P.lds_nodes; i += RT_BLOCK_BVH) {
       const float4 q = src[i];
@@ -173,7 +174,7 @@ __global__ __launch_bounds__(256) void rt_encode8_kernel(const float* __restrict
 
 static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
   return (variant & RT_VAR_BASE) == RT_VAR_FLAT ? 0
-                                                 : (size_t)stack_depth * RT_BLOCK_BVH * sizeof(int) + (size_t)lds_nodes * 64;
+                                                 : (size_t)(stack_depth + 1) * RT_BLOCK_BVH * sizeof(int) + (size_t)lds_nodes * 64;
 }
 
 // the kernel instantiation of a variant code (base variant | RT_VAR_NOISE)

@@ -627,6 +627,33 @@ RT_FN void trav_round(const KernelParams& P, const RayCtx& R, TravState& S, cons
     }
 #endif
     const bool hl = lnear <= lfar, hr = rnear <= rfar;
+#ifndef RT_BRANCHY_STACK
+    {
+      // Branch-free step: the stack slots a pop may need (sp-1, sp-2) are read and the far child
+      // is written to slot sp (free; slot stack_depth is a spare row) every step, and the next
+      // node / stack pointer are selects — no divergent branches around the LDS accesses.
+      const bool both = hl && hr, one = hl != hr;
+      const bool rfirst = rnear < lnear;
+      const int nearc = both ? (rfirst ? cr : cl) : (hl ? cl : cr);
+      const int farc = rfirst ? cl : cr;
+      const int sp = S.sp;
+      const int top1 = stack[(sp > 0 ? sp - 1 : 0) * stride];
+      const int top2 = stack[(sp > 1 ? sp - 2 : 0) * stride];
+      const bool room = sp < P.stack_depth;
+      stack[(room ? sp : P.stack_depth) * stride] = farc;
+      overflow |= (both && !room) ? 1 : 0;
+      int next = (both || one) ? nearc : (sp > 0 ? top1 : kDone);
+      int nsp = both ? (room ? sp + 1 : sp) : one ? sp : (sp > 0 ? sp - 1 : 0);
+      if (next < 0 && next != kDone && S.leaf == 0) {  // park the first leaf, keep descending
+        S.leaf = next;
+        const bool pushed = both && room;  // its pop is the far child just written
+        next = pushed ? farc : (both || one) ? (sp > 0 ? top1 : kDone) : (sp > 1 ? top2 : kDone);
+        nsp = pushed ? sp : (both || one) ? (sp > 0 ? sp - 1 : 0) : (sp > 1 ? sp - 2 : 0);
+      }
+      S.node = next;
+      S.sp = nsp;
+    }
+#else
     if (hl && hr) {
       const bool rfirst = rnear < lnear;
       const int nearc = rfirst ? cr : cl, farc = rfirst ? cl : cr;
@@ -646,6 +673,7 @@ RT_FN void trav_round(const KernelParams& P, const RayCtx& R, TravState& S, cons
       S.leaf = S.node;
       S.node = pop();
     }
+#endif
     if (!RT_ANY(S.leaf == 0)) break;  // every traversing lane holds a leaf
   }
   while (S.leaf < 0) {
