@@ -205,7 +205,9 @@ def main():
                 works[k] = None
         torch.cuda.synchronize(dev)
 
-    for _ in range(args.warmup):
+    # untimed warm-up: W frames, and at least one per stream (a stream's first frame pays for its
+    # stream-ordered allocation pool)
+    for _ in range(max(args.warmup, len(streams))):
         step(False)
     drain()
     if n > 1:
