@@ -45,7 +45,7 @@ inline int f2i(float f) {
 extern thread_local long long counters[4];
 }  // namespace rt_emu
 #define RT_F2I(f) rt_emu::f2i(f)
-#define RT_SINCOS(x, s, c) (*(s) = sinf(x), *(c) = cosf(x))
+#define RT_SINCOS_TURNS(x, s, c) (*(s) = sinf(6.283185307179586f * (x)), *(c) = cosf(6.283185307179586f * (x)))
 #define RT_LOG(x) logf(x)
 #define RT_RSQRT(x) (1.0f / sqrtf(x))
 #define RT_RCP(x) (1.0f / (x))
@@ -58,7 +58,8 @@ extern thread_local long long counters[4];
 #define RT_FN __device__ __forceinline__
 #define RT_FN_SPEC __device__ __forceinline__
 #define RT_F2I(f) __float_as_int(f)
-#define RT_SINCOS(x, s, c) __sincosf(x, s, c)
+// sin / cos of 2 pi x for x in [0, 1): v_sin_f32 / v_cos_f32 take their argument in turns
+#define RT_SINCOS_TURNS(x, s, c) (*(s) = __builtin_amdgcn_sinf(x), *(c) = __builtin_amdgcn_cosf(x))
 #define RT_LOG(x) __logf(x)
 #define RT_RSQRT(x) __frsqrt_rn(x)
 #define RT_RCP(x) __builtin_amdgcn_rcpf(x)
@@ -170,7 +171,7 @@ RT_FN f3 unit_vector(uint32_t a, uint32_t b) {
   c = 1.0f - 2.0f * u01(b);
   s = sqrtf(fmaxf(0.0f, 1.0f - c * c));
 #else
-  RT_SINCOS(2.0f * kPi * u01(b), &s, &c);
+  RT_SINCOS_TURNS(u01(b), &s, &c);
 #endif
   return mk3(r * c, r * s, z);
 }
@@ -322,14 +323,14 @@ RT_FN int box_field(int base, int code, int f, bool& present) {
   present = off != RT_BOX_NO_FACE;
   return base + off;
 }
-template <bool kKeyOnly>
-RT_FN void box_candidate(const RT_CAS DevBox* B, int f, float t, float q, const RayCtx& R, Closest& C) {
+// a face's key order, its primitive and whether the hit on it is valid (margin q >= 0, the face
+// exists, and it is not the face the ray leaves)
+RT_FN bool box_face(const RT_CAS DevBox* B, int f, float q, const RayCtx& R, int& ord, int& prim, bool with_prim) {
   bool present;
-  const int ord = box_field(B->ord_base, B->ord_code, f, present);
+  ord = box_field(B->ord_base, B->ord_code, f, present);
   const int gid = box_field(B->gid_base, B->gid_code, f, present);
-  int prim = 0;
-  if constexpr (!kKeyOnly) prim = box_field(B->prim_base, B->prim_code, f, present);
-  consider<kKeyOnly>(C, t, present && gid != R.self_gid ? q : -1.0f, ord, prim);
+  if (with_prim) prim = box_field(B->prim_base, B->prim_code, f, present);
+  return present && gid != R.self_gid && q >= 0.0f;
 }
 template <bool kKeyOnly>
 RT_FN void test_box(const RT_CAS DevBox* B, const RayCtx& R, float tmin_up, Closest& C) {
@@ -354,8 +355,12 @@ RT_FN void test_box(const RT_CAS DevBox* B, const RayCtx& R, float tmin_up, Clos
   const int fn = 2 * an + (an == 0 ? flip[0] : an == 1 ? flip[1] : flip[2]);
   const int ff = 2 * af + 1 - (af == 0 ? flip[0] : af == 1 ? flip[1] : flip[2]);
   const float gap = tf - tn;  // >= 0: the line meets the box
-  box_candidate<kKeyOnly>(B, fn, tn, fminf(gap, tn - tmin_up), R, C);
-  box_candidate<kKeyOnly>(B, ff, tf, fminf(gap, tf - tmin_up), R, C);
+  // the entry point is nearer than the exit point: the exit matters only when the entry is not
+  // a valid hit (one key compare per box)
+  int ord_n, ord_f, prim_n = 0, prim_f = 0;
+  const bool vn = box_face(B, fn, fminf(gap, tn - tmin_up), R, ord_n, prim_n, !kKeyOnly);
+  const bool vf = box_face(B, ff, fminf(gap, tf - tmin_up), R, ord_f, prim_f, !kKeyOnly);
+  consider<kKeyOnly>(C, vn ? tn : tf, (vn || vf) ? 0.0f : -1.0f, vn ? ord_n : ord_f, vn ? prim_n : prim_f);
 }
 
 // BVH scenes: the surface set's large-primitive prefix (rt_build.cpp; P.flat_sets[0]), tested
@@ -755,7 +760,7 @@ RT_FN void camera_ray(const KernelParams& P, uint32_t pix, int sample, int px, i
       P.cam.disk_v[1] != 0.0f || P.cam.disk_v[2] != 0.0f) {
     u4 w1 = philox(pix, (uint32_t)sample, 0u, RT_EV_CAMERA1, P.key0, P.key1);
     float rad = sqrtf(u01(w0.w)), s, c;
-    RT_SINCOS(2.0f * kPi * u01(w1.x), &s, &c);
+    RT_SINCOS_TURNS(u01(w1.x), &s, &c);
     origin = origin + (rad * c) * ld3(P.cam.disk_u) + (rad * s) * ld3(P.cam.disk_v);
   }
   f3 target = ld3(P.cam.top_left) + ((float)px + u01(w0.x)) * ld3(P.cam.pixel_u) +

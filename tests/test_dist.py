@@ -44,7 +44,7 @@ def _worker(rank, world, port, row_block, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,row_block", [(2, 4), (3, 3)])
+@pytest.mark.parametrize("world,row_block", [(2, 4), (3, 3), (2, 1)])
 def test_sharded_render_equals_single_render(emu_mod, tmp_path, world, row_block):
     out = str(tmp_path / "img.npy")
     mp.spawn(_worker, args=(world, _free_port(), row_block, out), nprocs=world, join=True)
