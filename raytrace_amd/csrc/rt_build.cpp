@@ -339,16 +339,57 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
           hi[a] = std::max(hi[a], b.hi[a]);
         }
       const double root_area = area(lo, hi);
+      double frac = RT_PREFIX_AREA;
+      if (const char* e = std::getenv("RT_AMD_PREFIX_AREA")) frac = atof(e);  // experiments
       std::vector<std::pair<double, int>> big;  // (area, position in sets[0])
       for (size_t j = 0; j < sets[0].size(); ++j) {
         const BuildPrim& b = sets[0][j];
         const double a = area(b.lo, b.hi);
-        if (sc->prims[b.index].motion < 0 && a >= RT_PREFIX_AREA * root_area) big.push_back({-a, (int)j});
+        if (sc->prims[b.index].motion < 0 && a >= frac * root_area) big.push_back({-a, (int)j});
       }
       std::stable_sort(big.begin(), big.end());
       if (big.size() > RT_PREFIX_MAX) big.resize(RT_PREFIX_MAX);
       std::vector<char> taken(sets[0].size(), 0);
       for (auto& b : big) taken[b.second] = 1;
+      // then outliers: a primitive that alone holds a face of the remaining set's box out by a
+      // lot (the Cornell light above the bunny: without it the BVH root shrinks to the bunny)
+      double shrink = RT_PREFIX_SHRINK;
+      if (const char* e = std::getenv("RT_AMD_PREFIX_SHRINK")) shrink = atof(e);  // experiments
+      for (int added = (int)big.size(); added < RT_PREFIX_MAX && shrink < 1.0; ++added) {
+        auto bounds_without = [&](int skip, double* l, double* h) {
+          for (int a = 0; a < 3; ++a) {
+            l[a] = INFINITY;
+            h[a] = -INFINITY;
+          }
+          for (size_t j = 0; j < sets[0].size(); ++j) {
+            if (taken[j] || (int)j == skip) continue;
+            for (int a = 0; a < 3; ++a) {
+              l[a] = std::min(l[a], sets[0][j].lo[a]);
+              h[a] = std::max(h[a], sets[0][j].hi[a]);
+            }
+          }
+        };
+        double l0[3], h0[3];
+        bounds_without(-1, l0, h0);
+        const double a0 = area(l0, h0);
+        int best_j = -1;
+        double best_a = a0;
+        for (size_t j = 0; j < sets[0].size(); ++j) {  // candidates: the primitives on the box's faces
+          const BuildPrim& b = sets[0][j];
+          bool extreme = false;
+          for (int a = 0; a < 3; ++a) extreme = extreme || b.lo[a] == l0[a] || b.hi[a] == h0[a];
+          if (taken[j] || !extreme || sc->prims[b.index].motion >= 0) continue;
+          double l[3], h[3];
+          bounds_without((int)j, l, h);
+          const double a = area(l, h);
+          if (a < best_a) {
+            best_a = a;
+            best_j = (int)j;
+          }
+        }
+        if (best_j < 0 || !(best_a <= (1.0 - shrink) * a0)) break;
+        taken[best_j] = 1;
+      }
       auto cls = [&](int i) {
         const int k = sc->prims[i].kind;
         return k == RT_PRIM_PARALLELOGRAM ? 0 : k == RT_PRIM_TRIANGLE ? 1 : 2;

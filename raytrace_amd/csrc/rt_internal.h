@@ -39,6 +39,9 @@
 #ifndef RT_PREFIX_AREA
 #define RT_PREFIX_AREA 0.1    // ... those whose box area is >= this fraction of the surface set's box
 #endif
+#ifndef RT_PREFIX_SHRINK
+#define RT_PREFIX_SHRINK 0.25 // ... and outliers whose removal shrinks the remaining box's area by this much
+#endif
 #ifndef RT_LDS_WG_BUDGET
 #define RT_LDS_WG_BUDGET 30720  // BVH kernel LDS per workgroup (stack + staged nodes): 5 per CU
 #endif
