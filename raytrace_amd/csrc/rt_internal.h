@@ -43,7 +43,7 @@
 #define RT_PREFIX_SHRINK 0.25 // ... and outliers whose removal shrinks the remaining box's area by this much
 #endif
 #ifndef RT_LDS_WG_BUDGET
-#define RT_LDS_WG_BUDGET 30720  // BVH kernel LDS per workgroup (stack + staged nodes): 5 per CU
+#define RT_LDS_WG_BUDGET 31744  // BVH kernel LDS per workgroup (stack + staged nodes): 5 per CU (32512 drops to 4)
 #endif
 #define RT_EMPTY_ROOT ((int)0x80000000)
 
