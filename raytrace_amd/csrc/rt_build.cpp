@@ -791,12 +791,14 @@ void rt_host_plan_work(KernelParams& P, long long resident_lanes) {
   // short; below ~2 samples the per-item commit (3 atomics) dominates.  Measured on MI355X,
   // Cornell 600x600x200 (tools/sweep_chunk.sh, an early kernel): 1 -> 14.3 ms, 2 -> 8.70, 4 -> 8.79, 8 -> 8.97,
   // 34 -> 10.3, 200 -> 16.5.  The image does not depend on this choice (fixed-point sums).
-  (void)resident_lanes;
   const long long tile_pixels = (long long)P.tile_rows * P.cam.width;
   const int spp = P.cam.spp;
-  // At 1000+ spp (bunny-Cornell, pawn+fog) 16-sample items cut the commit atomics 4x: -2.4 % /
-  // -1 % there, while the Cornell box (200 spp) is fastest at 4 and demo1 (500) indifferent.
-  int chunk = spp < 4 ? spp : spp >= 800 ? 16 : 4;
+  // 16-sample items cut the commit atomics 4x where every lane still runs many items (bunny-
+  // Cornell / pawn+fog at 1 GPU: -2.4 % / -1 %); with fewer than ~64 items per resident lane (an
+  // 8-GPU rank's share, the Cornell box) the longer last items cost more than that (bunny at 8
+  // shards: 20.7 -> 22.0 ms), so those keep 4.
+  int chunk = spp < 4 ? spp : 4;
+  if (resident_lanes > 0 && (long long)P.tile_rows * P.cam.width * spp / 16 >= 64 * resident_lanes) chunk = 16;
   if (const char* env = std::getenv("RT_AMD_CHUNK")) {  // tuning knob for experiments
     int c = std::atoi(env);
     if (c > 0) chunk = c;
