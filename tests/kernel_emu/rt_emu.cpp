@@ -156,6 +156,16 @@ int rt_emu_scene_info(const rt_scene* sc, int* info) {
   info[2] = H.max_depth;
   info[3] = H.n_prims;
   info[4] = H.flat ? 1 : 0;
+  info[5] = (int)H.boxes.size();
+  // BVH scenes: primitives tested before the surface BVH (prefix records + box-group faces)
+  int pre = 0;
+  if (!H.flat) {
+    const DevFlatSet& F = H.flat_sets[0];
+    pre = F.end - F.first;
+    for (int b = F.box_first; b < F.box_end; ++b)
+      for (int f = 0; f < 6; ++f) pre += ((H.boxes[b].ord_code >> (5 * f)) & 31) != RT_BOX_NO_FACE;
+  }
+  info[6] = pre;
   return RT_OK;
 }
 }

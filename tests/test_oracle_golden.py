@@ -327,3 +327,14 @@ def test_oracle_edge_cases(oracle_mod):
     # width-1 image
     one = oracle_mod.render(cs.replace(cs_imageWidth=1), world, seed)
     assert one.shape == (1, 1, 3)
+
+
+@pytest.mark.parametrize("name,boxes,prefix", [("cornell", 3, 0), ("box_gallery", 4, 0), ("bunny_cornell", 1, 6),
+                                               ("demo1", 0, 1), ("pawn_fog", 0, 0), ("readme", 0, 0)])
+def test_host_build_box_groups_and_prefix(emu_mod, name, boxes, prefix):
+    """The host build finds the box groups (the Cornell walls = 5 faces of the 555-cube, every
+    `cuboid`) and the BVH scenes' surface prefix (the walls and the light around the bunny,
+    demo1's ground sphere; nothing for the pawn's triangles)."""
+    cs, world, seed = scenes.CONFIGS[name]()
+    info = emu_mod.scene_info(world)
+    assert info["boxes"] == boxes and info["prefix"] == prefix, info
