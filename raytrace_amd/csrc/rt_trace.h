@@ -165,11 +165,11 @@ RT_FN float u01(uint32_t w) { return (float)(w >> 8) * (1.0f / 16777216.0f); }
 // uniform direction on the unit sphere (the distribution of randomUnitVector, Core.hs:54-60)
 RT_FN f3 unit_vector(uint32_t a, uint32_t b) {
   float z = 1.0f - 2.0f * u01(a);
-  float r = sqrtf(fmaxf(0.0f, 1.0f - z * z));
+  float r = RT_SQRT(fmaxf(0.0f, 1.0f - z * z));
   float s, c;
 #ifdef RT_EXP_NO_SINCOS  // ablation: wrong directions, measures the cost of sincos
   c = 1.0f - 2.0f * u01(b);
-  s = sqrtf(fmaxf(0.0f, 1.0f - c * c));
+  s = RT_SQRT(fmaxf(0.0f, 1.0f - c * c));
 #else
   RT_SINCOS_TURNS(u01(b), &s, &c);
 #endif
@@ -759,7 +759,7 @@ RT_FN void camera_ray(const KernelParams& P, uint32_t pix, int sample, int px, i
   if (P.cam.disk_u[0] != 0.0f || P.cam.disk_u[1] != 0.0f || P.cam.disk_u[2] != 0.0f || P.cam.disk_v[0] != 0.0f ||
       P.cam.disk_v[1] != 0.0f || P.cam.disk_v[2] != 0.0f) {
     u4 w1 = philox(pix, (uint32_t)sample, 0u, RT_EV_CAMERA1, P.key0, P.key1);
-    float rad = sqrtf(u01(w0.w)), s, c;
+    float rad = RT_SQRT(u01(w0.w)), s, c;
     RT_SINCOS_TURNS(u01(w1.x), &s, &c);
     origin = origin + (rad * c) * ld3(P.cam.disk_u) + (rad * s) * ld3(P.cam.disk_v);
   }
@@ -865,7 +865,7 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
       float ior = Mt.param;
       float ratio = h.front ? RT_RCP(ior) : ior;
       float cos_t = fminf(1.0f, -dot(h.n, R.d));
-      float sin_t = sqrtf(fmaxf(0.0f, 1.0f - cos_t * cos_t));
+      float sin_t = RT_SQRT(fmaxf(0.0f, 1.0f - cos_t * cos_t));
       float r0 = (1.0f - ratio) * RT_RCP(1.0f + ratio);
       r0 = r0 * r0;
       float x1 = 1.0f - cos_t, x2 = x1 * x1;
@@ -874,7 +874,7 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
         newdir = unit(reflect(h.n, R.d));
       } else {
         f3 perp = ratio * (R.d + cos_t * h.n);
-        newdir = unit(perp - sqrtf(fabsf(1.0f - dot(perp, perp))) * h.n);
+        newdir = unit(perp - RT_SQRT(fabsf(1.0f - dot(perp, perp))) * h.n);
       }
       break;
     }
@@ -919,7 +919,7 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
       } else if (Mt.kind == 9) {
         float g = Mt.param, mu = dot(R.d, dir);
         float base = 1.0f + g * g - 2.0f * g * mu;
-        f = ((1.0f - g * g) * RT_RCP(base * sqrtf(base))) * f;
+        f = ((1.0f - g * g) * RT_RCP(base * RT_SQRT(base))) * f;
       }
       T = T * ((pdf1 * RT_RCP(pdf)) * f);
       newdir = dir;
