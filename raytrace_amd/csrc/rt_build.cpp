@@ -683,14 +683,13 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
 }
 
 int rt_host_variant(bool flat, int n_media, bool noise) {
-  (void)n_media;  // the decoupled loop measured faster with and without media
   int v = flat ? RT_VAR_FLAT : RT_VAR_BVH;
   if (const char* e = std::getenv("RT_AMD_VARIANT")) {
     const int f = atoi(e);
     if (!flat && (f == RT_VAR_BVH_LOCKSTEP || f == RT_VAR_BVH)) v = f;  // flat scenes run on any variant
     if (flat && f >= RT_VAR_FLAT && f <= RT_VAR_BVH) v = f;
   }
-  return v | (noise ? RT_VAR_NOISE : 0);
+  return v | (noise ? RT_VAR_NOISE : 0) | (n_media > 0 ? RT_VAR_MEDIA : 0);
 }
 
 int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex, KernelParams& P,

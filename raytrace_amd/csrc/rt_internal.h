@@ -53,6 +53,7 @@
 #define RT_VAR_BVH 2           // BVH, traversal decoupled from shading (default for BVH scenes)
 #define RT_VAR_BASE 3
 #define RT_VAR_NOISE 4         // flag: the scene has noise / marble textures (their code compiled in)
+#define RT_VAR_MEDIA 8         // flag: the scene has constantMedium volumes (their code compiled in)
 // workgroup size of a variant's render kernel
 inline int rt_block_of(int variant) { return (variant & RT_VAR_BASE) == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH; }
 // host choice of variant (rt_build.cpp); env RT_AMD_VARIANT overrides the base for experiments

@@ -971,7 +971,7 @@ RT_FN bool open_item(const KernelParams& P, int item, ItemCtx& I) {
 // for lanes with need == true.  `commit(tile_pixel, sx, sy, sz, bad)` adds a finished item's
 // sums.  One segment per iteration, all of its queries run by the whole wave together: the flat
 // kernel (every lane tests the same primitives) and the BVH kernel of scenes with media.
-template <bool kFlat, bool kNoise, class Grab, class Commit>
+template <bool kFlat, bool kNoise, bool kMedia, class Grab, class Commit>
 RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW,
                              const float* prims_) {
   const cfp prims = cf(prims_);
@@ -1011,7 +1011,9 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
     float tbest = C.t;
     const int best = C.prim;
     int hit_medium = -1;
-    for (int m = 0; m < P.n_media; ++m) {
+    // media: compiled only into the instantiations for scenes that have them (kMedia)
+    const int n_media = kMedia ? P.n_media : 0;
+    for (int m = 0; m < n_media; ++m) {
       // constantMedium (Geometry.hs:306-328)
       const DevMedium& M = P.media[m];
       Closest C1 = no_hit();
@@ -1060,9 +1062,10 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
 // entering it, the second (Geometry.hs:306-328) — each starting inside the traversal loop as
 // soon as the previous one finishes.
 enum : int { ST_NEED_ITEM = 0, ST_NEED_SAMPLE = 1, ST_START_SEG = 2, ST_TRACE = 3, ST_SHADE = 4 };
-template <bool kNoise, class Grab, class Commit>
+template <bool kNoise, bool kMedia, class Grab, class Commit>
 RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW, const float* prims_) {
   const cfp prims = cf(prims_);
+  const int n_media = kMedia ? P.n_media : 0;  // media code only in the kMedia instantiations
   int overflow = 0;
   ItemCtx I{-1, 0, 0, 0, 0, 0, 0u};
   int seg = 0;
@@ -1144,13 +1147,13 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
             }
           }
           // media whose boundary is the surface set reuse the surface hit (DevMedium)
-          while (next_m >= 0 && next_m < P.n_media && P.media[next_m].alias_surface) {
+          while (next_m >= 0 && next_m < n_media && P.media[next_m].alias_surface) {
             if (best >= 0 && !prim_front(P, prims, best, R, t_surf))
               medium_event(P, next_m, I.pix, I.sample, seg, kTmin, t_surf, tbest, hit_medium);
             ++next_m;
           }
           if (next_m >= 0) {
-            if (next_m < P.n_media) {
+            if (next_m < n_media) {
               q = 1 + 2 * next_m;
               trav_begin(S, P.media[next_m].root, kTmin);
             } else {

@@ -44,6 +44,20 @@ struct Commit {
   }
 };
 
+template <bool kNoise, bool kMedia, class G, class Cm>
+int run_loop(const KernelParams& P, int base, G& g, Cm& c, const rtk::Trav& W) {
+  switch (base) {
+    case RT_VAR_FLAT: return rtk::lane_loop_lockstep<true, kNoise, kMedia>(P, g, c, W, P.prims);
+    case RT_VAR_BVH_LOCKSTEP: return rtk::lane_loop_lockstep<false, kNoise, kMedia>(P, g, c, W, P.prims);
+    default: return rtk::lane_loop_bvh<kNoise, kMedia>(P, g, c, W, P.prims);
+  }
+}
+template <class G, class Cm>
+int run_variant(const KernelParams& P, int base, bool noise, bool media, G& g, Cm& c, const rtk::Trav& W) {
+  if (noise) return media ? run_loop<true, true>(P, base, g, c, W) : run_loop<true, false>(P, base, g, c, W);
+  return media ? run_loop<false, true>(P, base, g, c, W) : run_loop<false, false>(P, base, g, c, W);
+}
+
 void* worker(void* arg) {
   Shared* s = (Shared*)arg;
   std::vector<int> stack(s->P->stack_depth + 1);
@@ -52,20 +66,8 @@ void* worker(void* arg) {
   Commit c{s};
   const rtk::Trav W{stack.data(), 1, nullptr};  // the emulator reads every node from memory
   int ov = 0;
-  const bool noise = (s->variant & RT_VAR_NOISE) != 0;
-  switch (s->variant & RT_VAR_BASE) {
-    case RT_VAR_FLAT:
-      ov = noise ? rtk::lane_loop_lockstep<true, true>(*s->P, g, c, W, s->P->prims)
-                 : rtk::lane_loop_lockstep<true, false>(*s->P, g, c, W, s->P->prims);
-      break;
-    case RT_VAR_BVH_LOCKSTEP:
-      ov = noise ? rtk::lane_loop_lockstep<false, true>(*s->P, g, c, W, s->P->prims)
-                 : rtk::lane_loop_lockstep<false, false>(*s->P, g, c, W, s->P->prims);
-      break;
-    default:
-      ov = noise ? rtk::lane_loop_bvh<true>(*s->P, g, c, W, s->P->prims)
-                 : rtk::lane_loop_bvh<false>(*s->P, g, c, W, s->P->prims);
-  }
+  const bool noise = (s->variant & RT_VAR_NOISE) != 0, media = (s->variant & RT_VAR_MEDIA) != 0;
+  ov = run_variant(*s->P, s->variant & RT_VAR_BASE, noise, media, g, c, W);
   if (ov)
     s->overflow = 1;
   for (int i = 0; i < 4; ++i) s->cnt[i] += rt_emu::counters[i];
