@@ -44,18 +44,25 @@ struct Commit {
   }
 };
 
-template <bool kNoise, bool kMedia, class G, class Cm>
+template <bool kNoise, bool kMedia, bool kMats, class G, class Cm>
 int run_loop(const KernelParams& P, int base, G& g, Cm& c, const rtk::Trav& W) {
   switch (base) {
-    case RT_VAR_FLAT: return rtk::lane_loop_lockstep<true, kNoise, kMedia>(P, g, c, W, P.prims);
-    case RT_VAR_BVH_LOCKSTEP: return rtk::lane_loop_lockstep<false, kNoise, kMedia>(P, g, c, W, P.prims);
-    default: return rtk::lane_loop_bvh<kNoise, kMedia>(P, g, c, W, P.prims);
+    case RT_VAR_FLAT: return rtk::lane_loop_lockstep<true, kNoise, kMedia, kMats>(P, g, c, W, P.prims);
+    case RT_VAR_BVH_LOCKSTEP: return rtk::lane_loop_lockstep<false, kNoise, kMedia, kMats>(P, g, c, W, P.prims);
+    default: return rtk::lane_loop_bvh<kNoise, kMedia, kMats>(P, g, c, W, P.prims);
   }
 }
+template <bool kNoise, bool kMedia, class G, class Cm>
+int run_mats(const KernelParams& P, int base, bool mats, G& g, Cm& c, const rtk::Trav& W) {
+  return mats ? run_loop<kNoise, kMedia, true>(P, base, g, c, W) : run_loop<kNoise, kMedia, false>(P, base, g, c, W);
+}
 template <class G, class Cm>
-int run_variant(const KernelParams& P, int base, bool noise, bool media, G& g, Cm& c, const rtk::Trav& W) {
-  if (noise) return media ? run_loop<true, true>(P, base, g, c, W) : run_loop<true, false>(P, base, g, c, W);
-  return media ? run_loop<false, true>(P, base, g, c, W) : run_loop<false, false>(P, base, g, c, W);
+int run_variant(const KernelParams& P, int variant, G& g, Cm& c, const rtk::Trav& W) {
+  const int base = variant & RT_VAR_BASE;
+  const bool noise = (variant & RT_VAR_NOISE) != 0, media = (variant & RT_VAR_MEDIA) != 0;
+  const bool mats = (variant & RT_VAR_MATS) != 0;
+  if (noise) return media ? run_mats<true, true>(P, base, mats, g, c, W) : run_mats<true, false>(P, base, mats, g, c, W);
+  return media ? run_mats<false, true>(P, base, mats, g, c, W) : run_mats<false, false>(P, base, mats, g, c, W);
 }
 
 void* worker(void* arg) {
@@ -66,8 +73,7 @@ void* worker(void* arg) {
   Commit c{s};
   const rtk::Trav W{stack.data(), 1, nullptr};  // the emulator reads every node from memory
   int ov = 0;
-  const bool noise = (s->variant & RT_VAR_NOISE) != 0, media = (s->variant & RT_VAR_MEDIA) != 0;
-  ov = run_variant(*s->P, s->variant & RT_VAR_BASE, noise, media, g, c, W);
+  ov = run_variant(*s->P, s->variant, g, c, W);
   if (ov)
     s->overflow = 1;
   for (int i = 0; i < 4; ++i) s->cnt[i] += rt_emu::counters[i];
@@ -121,7 +127,7 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
   for (auto& f : flags) f = 0;
   Shared s;
   s.P = &P;
-  s.variant = rt_host_variant(H.flat, H.n_media, H.noise);
+  s.variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats);
   s.accum = &accum;
   s.flags = &flags;
   for (auto& c : s.cnt) c = 0;
