@@ -151,7 +151,7 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
   s->n_prims = H.n_prims;
   s->max_depth = H.max_depth;
   s->stack_depth = H.max_depth > 1 ? H.max_depth : 1;
-  s->variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats);
+  s->variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex);
   if ((s->variant & RT_VAR_BASE) != RT_VAR_FLAT) {
     // stage as many top (breadth-first) surface nodes as fit beside the stacks in the per-
     // workgroup budget; env RT_AMD_LDS_NODES caps it (0 disables, for experiments)

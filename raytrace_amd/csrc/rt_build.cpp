@@ -231,9 +231,11 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
       if (!finite_n(sc->perlin->grad[k], 3)) return fail(err, RT_E_INVALID, "non-finite perlin gradient");
   }
   S.full_mats = false;
+  S.uv_tex = false;
   for (int i = 0; i < sc->n_materials; ++i) {
     const rt_material& m = sc->materials[i];
     if (m.kind != RT_MAT_LIGHT_SOURCE && m.kind != RT_MAT_PITCH_BLACK && m.kind != RT_MAT_LAMBERTIAN) S.full_mats = true;
+    if (m.texture >= 0 && m.texture < sc->n_textures && sc->textures[m.texture].kind != RT_TEX_CONSTANT) S.uv_tex = true;
     if (m.kind < 0 || m.kind > RT_MAT_ANISOTROPIC)
       return fail(err, RT_E_UNSUPPORTED, "material %d: kind %d", i, m.kind);
     if (m.texture < 0 || m.texture >= sc->n_textures)
@@ -684,14 +686,15 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   return RT_OK;
 }
 
-int rt_host_variant(bool flat, int n_media, bool noise, bool mats) {
+int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex) {
   int v = flat ? RT_VAR_FLAT : RT_VAR_BVH;
   if (const char* e = std::getenv("RT_AMD_VARIANT")) {
     const int f = atoi(e);
     if (!flat && (f == RT_VAR_BVH_LOCKSTEP || f == RT_VAR_BVH)) v = f;  // flat scenes run on any variant
     if (flat && f >= RT_VAR_FLAT && f <= RT_VAR_BVH) v = f;
   }
-  return v | (noise ? RT_VAR_NOISE : 0) | (n_media > 0 ? RT_VAR_MEDIA : 0) | (mats ? RT_VAR_MATS : 0);
+  return v | (noise ? RT_VAR_NOISE : 0) | (n_media > 0 ? RT_VAR_MEDIA : 0) | (mats ? RT_VAR_MATS : 0) |
+         (tex ? RT_VAR_TEX : 0);
 }
 
 int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex, KernelParams& P,

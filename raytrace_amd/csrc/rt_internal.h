@@ -55,10 +55,11 @@
 #define RT_VAR_NOISE 4         // flag: the scene has noise / marble textures (their code compiled in)
 #define RT_VAR_MEDIA 8         // flag: the scene has constantMedium volumes (their code compiled in)
 #define RT_VAR_MATS 16         // flag: materials beyond lightSource / pitchBlack / lambertian
+#define RT_VAR_TEX 32          // flag: some material reads a non-constant texture
 // workgroup size of a variant's render kernel
 inline int rt_block_of(int variant) { return (variant & RT_VAR_BASE) == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH; }
 // host choice of variant (rt_build.cpp); env RT_AMD_VARIANT overrides the base for experiments
-int rt_host_variant(bool flat, int n_media, bool noise, bool mats);
+int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex);
 
 #define RT_KIND_MASK 3
 #define RT_FLAG_MOTION 4
@@ -232,6 +233,7 @@ struct HostScene {
   int surface_nodes = 0;  // nodes of the surface BVH: [0, surface_nodes), breadth-first
   bool flat = false;  // every set is a single flat leaf (no BVH nodes)
   bool noise = false;  // some texture is a noise / marble texture
+  bool uv_tex = false;     // some material reads a non-constant texture (RT_VAR_TEX)
   bool full_mats = false;  // some material is not lightSource / pitchBlack / lambertian (RT_VAR_MATS)
 };
 

@@ -92,9 +92,9 @@ struct AtomicCommit {
 #ifndef RT_WAVES_BVH
 #define RT_WAVES_BVH 5
 #endif
-template <int kVar, bool kNoise, bool kMedia, bool kMats>
+template <int kVar, int kTex, bool kMedia, bool kMats>
 __global__ __launch_bounds__(kVar == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH)
-__attribute__((amdgpu_waves_per_eu(kVar == RT_VAR_FLAT ? (kNoise ? RT_WAVES_FLAT_NOISE : RT_WAVES_FLAT)
+__attribute__((amdgpu_waves_per_eu(kVar == RT_VAR_FLAT ? (kTex == 2 ? RT_WAVES_FLAT_NOISE : RT_WAVES_FLAT)
                                                          : RT_WAVES_BVH)))
 void rt_render_kernel(KernelParams P) {
   extern __shared__ int smem[];
@@ -107,7 +107,7 @@ void rt_render_kernel(KernelParams P) {
   int overflow;
   if constexpr (kVar == RT_VAR_FLAT) {
     overflow =
-        rtk::lane_loop_lockstep<true, kNoise, kMedia, kMats>(P, grab, commit, rtk::Trav{nullptr, 0, nullptr}, P.prims);
+        rtk::lane_loop_lockstep<true, kTex, kMedia, kMats>(P, grab, commit, rtk::Trav{nullptr, 0, nullptr}, P.prims);
   } else {
     // LDS: [stack_depth + 1][RT_BLOCK_BVH] stack words (the last row a spare write target), then
     // the top P.lds_nodes BVH nodes (64 B each)
@@ -120,9 +120,9 @@ void rt_render_kernel(KernelParams P) {
     __syncthreads();
     const rtk::Trav W{smem + threadIdx.x, RT_BLOCK_BVH, lds_nodes};
     if constexpr (kVar == RT_VAR_BVH_LOCKSTEP)
-      overflow = rtk::lane_loop_lockstep<false, kNoise, kMedia, kMats>(P, grab, commit, W, P.prims);
+      overflow = rtk::lane_loop_lockstep<false, kTex, kMedia, kMats>(P, grab, commit, W, P.prims);
     else
-      overflow = rtk::lane_loop_bvh<kNoise, kMedia, kMats>(P, grab, commit, W, P.prims);
+      overflow = rtk::lane_loop_bvh<kTex, kMedia, kMats>(P, grab, commit, W, P.prims);
   }
   if (overflow) atomicOr(P.status, 1);
 }
@@ -181,21 +181,27 @@ static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
                                                  : (size_t)(stack_depth + 1) * RT_BLOCK_BVH * sizeof(int) + (size_t)lds_nodes * 64;
 }
 
-// the kernel instantiation of a variant code (base variant | RT_VAR_NOISE | RT_VAR_MEDIA |
-// RT_VAR_MATS): noise textures, media and the materials beyond lightSource / pitchBlack /
-// lambertian are compiled only into the instantiations of scenes that use them
+// the kernel instantiation of a variant code (base variant | RT_VAR_TEX | RT_VAR_NOISE |
+// RT_VAR_MEDIA | RT_VAR_MATS): non-constant textures, noise textures, media and the materials
+// beyond lightSource / pitchBlack / lambertian are compiled only into the instantiations of
+// scenes that use them
 // (inlined everywhere it raises the register allocation of every scene's kernel: the Cornell
 // box is 4.8 % faster without the unused media code)
 typedef void (*render_fn)(KernelParams);
-template <int kVar, bool kNoise, bool kMedia>
+template <int kVar, int kTex, bool kMedia>
 static render_fn render_kernel_mats(int variant) {
-  return (variant & RT_VAR_MATS) ? rt_render_kernel<kVar, kNoise, kMedia, true> : rt_render_kernel<kVar, kNoise, kMedia, false>;
+  return (variant & RT_VAR_MATS) ? rt_render_kernel<kVar, kTex, kMedia, true> : rt_render_kernel<kVar, kTex, kMedia, false>;
+}
+template <int kVar, int kTex>
+static render_fn render_kernel_media(int variant) {
+  return (variant & RT_VAR_MEDIA) ? render_kernel_mats<kVar, kTex, true>(variant)
+                                  : render_kernel_mats<kVar, kTex, false>(variant);
 }
 template <int kVar>
 static render_fn render_kernel_flags(int variant) {
-  const bool noise = (variant & RT_VAR_NOISE) != 0, media = (variant & RT_VAR_MEDIA) != 0;
-  return noise ? (media ? render_kernel_mats<kVar, true, true>(variant) : render_kernel_mats<kVar, true, false>(variant))
-               : (media ? render_kernel_mats<kVar, false, true>(variant) : render_kernel_mats<kVar, false, false>(variant));
+  if (variant & RT_VAR_NOISE) return render_kernel_media<kVar, 2>(variant);
+  if (variant & RT_VAR_TEX) return render_kernel_media<kVar, 1>(variant);
+  return render_kernel_media<kVar, 0>(variant);
 }
 static render_fn render_kernel_of(int variant) {
   switch (variant & RT_VAR_BASE) {

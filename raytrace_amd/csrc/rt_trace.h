@@ -802,7 +802,7 @@ RT_FN void medium_event(const KernelParams& P, int m, uint32_t pix, int sample, 
 // (and seg).  Returns true when the path terminates.
 // kMats: the scene has materials beyond lightSource / pitchBlack / lambertian; their code is
 // compiled only into those instantiations (the Cornell box and the bunny have none: -2.4 % / -1.2 %)
-template <bool kNoise, bool kMats>
+template <int kTex, bool kMats>
 RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int& seg, float tbest, int best,
                  int hit_medium, RayCtx& R, f3& L, f3& T) {
   RT_HOOK_SEGMENT(pix, sample, seg, R, tbest, best, hit_medium, L, T);
@@ -824,7 +824,9 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
   const DevMaterial Mt = DevMaterial{Mp->kind, Mp->tex, Mp->param, Mp->tex_const, {0.f, 0.f, 0.f}, 0.f};
   // every material but pitchBlack and dielectric reads its texture; constant textures come with
   // the record, the others are evaluated once (one inlined copy keeps the register allocation down)
-  const bool need_tex = !Mt.tex_const && Mt.kind != RT_MAT_PITCH_BLACK && Mt.kind != RT_MAT_DIELECTRIC;
+  // (kTex: 0 — every texture is constant, the texture code is not compiled in; 1 — uv / image
+  // textures; 2 — noise / marble textures too)
+  const bool need_tex = kTex > 0 && !Mt.tex_const && Mt.kind != RT_MAT_PITCH_BLACK && Mt.kind != RT_MAT_DIELECTRIC;
   HitInfo h;
   if (hit_medium >= 0) {
     h.p = R.o + tbest * R.d;
@@ -837,7 +839,7 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
     h = surface_info(P, prims, best, R, tbest, need_tex);
   }
   f3 tex = f3{Mp->c0[0], Mp->c0[1], Mp->c0[2]};
-  if (need_tex) tex = eval_texture<kNoise>(P, Mt.tex, h.u, h.v, h.p);
+  if (need_tex) tex = eval_texture<kTex == 2>(P, Mt.tex, h.u, h.v, h.p);
   u4 w = philox(pix, (uint32_t)sample, (uint32_t)seg, RT_EV_SCATTER, P.key0, P.key1);
   const bool last = seg + 1 >= P.cam.max_depth;  // rayColor (depth - 1) with depth - 1 <= 0 is zero
   f3 newdir = R.d;
@@ -978,7 +980,7 @@ RT_FN bool open_item(const KernelParams& P, int item, ItemCtx& I) {
 // for lanes with need == true.  `commit(tile_pixel, sx, sy, sz, bad)` adds a finished item's
 // sums.  One segment per iteration, all of its queries run by the whole wave together: the flat
 // kernel (every lane tests the same primitives) and the BVH kernel of scenes with media.
-template <bool kFlat, bool kNoise, bool kMedia, bool kMats, class Grab, class Commit>
+template <bool kFlat, int kTex, bool kMedia, bool kMats, class Grab, class Commit>
 RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW,
                              const float* prims_) {
   const cfp prims = cf(prims_);
@@ -1046,7 +1048,7 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
       }
       medium_event(P, m, I.pix, I.sample, seg, lo, hi, tbest, hit_medium);
     }
-    if (shade<kNoise, kMats>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T)) {
+    if (shade<kTex, kMats>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T)) {
       RT_HOOK_SAMPLE(I.pix, I.sample, L);
       sx += to_fixed(L.x, bad);
       sy += to_fixed(L.y, bad);
@@ -1069,7 +1071,7 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
 // entering it, the second (Geometry.hs:306-328) — each starting inside the traversal loop as
 // soon as the previous one finishes.
 enum : int { ST_NEED_ITEM = 0, ST_NEED_SAMPLE = 1, ST_START_SEG = 2, ST_TRACE = 3, ST_SHADE = 4 };
-template <bool kNoise, bool kMedia, bool kMats, class Grab, class Commit>
+template <int kTex, bool kMedia, bool kMats, class Grab, class Commit>
 RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW, const float* prims_) {
   const cfp prims = cf(prims_);
   const int n_media = kMedia ? P.n_media : 0;  // media code only in the kMedia instantiations
@@ -1175,7 +1177,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
     }
     // ---- shade the segments whose queries are complete
     if (state == ST_SHADE) {
-      if (shade<kNoise, kMats>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T)) {
+      if (shade<kTex, kMats>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T)) {
         RT_HOOK_SAMPLE(I.pix, I.sample, L);
         sx += to_fixed(L.x, bad);
         sy += to_fixed(L.y, bad);

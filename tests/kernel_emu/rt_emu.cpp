@@ -44,25 +44,26 @@ struct Commit {
   }
 };
 
-template <bool kNoise, bool kMedia, bool kMats, class G, class Cm>
+template <int kTex, bool kMedia, bool kMats, class G, class Cm>
 int run_loop(const KernelParams& P, int base, G& g, Cm& c, const rtk::Trav& W) {
   switch (base) {
-    case RT_VAR_FLAT: return rtk::lane_loop_lockstep<true, kNoise, kMedia, kMats>(P, g, c, W, P.prims);
-    case RT_VAR_BVH_LOCKSTEP: return rtk::lane_loop_lockstep<false, kNoise, kMedia, kMats>(P, g, c, W, P.prims);
-    default: return rtk::lane_loop_bvh<kNoise, kMedia, kMats>(P, g, c, W, P.prims);
+    case RT_VAR_FLAT: return rtk::lane_loop_lockstep<true, kTex, kMedia, kMats>(P, g, c, W, P.prims);
+    case RT_VAR_BVH_LOCKSTEP: return rtk::lane_loop_lockstep<false, kTex, kMedia, kMats>(P, g, c, W, P.prims);
+    default: return rtk::lane_loop_bvh<kTex, kMedia, kMats>(P, g, c, W, P.prims);
   }
 }
-template <bool kNoise, bool kMedia, class G, class Cm>
-int run_mats(const KernelParams& P, int base, bool mats, G& g, Cm& c, const rtk::Trav& W) {
-  return mats ? run_loop<kNoise, kMedia, true>(P, base, g, c, W) : run_loop<kNoise, kMedia, false>(P, base, g, c, W);
+template <int kTex, class G, class Cm>
+int run_flags(const KernelParams& P, int variant, G& g, Cm& c, const rtk::Trav& W) {
+  const int base = variant & RT_VAR_BASE;
+  const bool media = (variant & RT_VAR_MEDIA) != 0, mats = (variant & RT_VAR_MATS) != 0;
+  if (media) return mats ? run_loop<kTex, true, true>(P, base, g, c, W) : run_loop<kTex, true, false>(P, base, g, c, W);
+  return mats ? run_loop<kTex, false, true>(P, base, g, c, W) : run_loop<kTex, false, false>(P, base, g, c, W);
 }
 template <class G, class Cm>
 int run_variant(const KernelParams& P, int variant, G& g, Cm& c, const rtk::Trav& W) {
-  const int base = variant & RT_VAR_BASE;
-  const bool noise = (variant & RT_VAR_NOISE) != 0, media = (variant & RT_VAR_MEDIA) != 0;
-  const bool mats = (variant & RT_VAR_MATS) != 0;
-  if (noise) return media ? run_mats<true, true>(P, base, mats, g, c, W) : run_mats<true, false>(P, base, mats, g, c, W);
-  return media ? run_mats<false, true>(P, base, mats, g, c, W) : run_mats<false, false>(P, base, mats, g, c, W);
+  if (variant & RT_VAR_NOISE) return run_flags<2>(P, variant, g, c, W);
+  if (variant & RT_VAR_TEX) return run_flags<1>(P, variant, g, c, W);
+  return run_flags<0>(P, variant, g, c, W);
 }
 
 void* worker(void* arg) {
@@ -127,7 +128,7 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
   for (auto& f : flags) f = 0;
   Shared s;
   s.P = &P;
-  s.variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats);
+  s.variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex);
   s.accum = &accum;
   s.flags = &flags;
   for (auto& c : s.cnt) c = 0;
