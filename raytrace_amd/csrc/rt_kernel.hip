@@ -92,10 +92,19 @@ struct AtomicCommit {
 #ifndef RT_WAVES_BVH
 #define RT_WAVES_BVH 5
 #endif
+// knobs for the lightest instantiations (constant textures; BVH: no media): measured, 8 waves
+// for the Cornell kernel (62 VGPRs, 6 spilled) -0.3..0.7 %, 6 for the bunny's (80, 4 spilled) +3.4 %
+#ifndef RT_WAVES_FLAT_TEX0
+#define RT_WAVES_FLAT_TEX0 7
+#endif
+#ifndef RT_WAVES_BVH_LITE
+#define RT_WAVES_BVH_LITE 5
+#endif
 template <int kVar, int kTex, bool kMedia, bool kMats>
 __global__ __launch_bounds__(kVar == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH)
-__attribute__((amdgpu_waves_per_eu(kVar == RT_VAR_FLAT ? (kTex == 2 ? RT_WAVES_FLAT_NOISE : RT_WAVES_FLAT)
-                                                         : RT_WAVES_BVH)))
+__attribute__((amdgpu_waves_per_eu(kVar == RT_VAR_FLAT ? (kTex == 2 ? RT_WAVES_FLAT_NOISE
+                                                                      : kTex == 0 ? RT_WAVES_FLAT_TEX0 : RT_WAVES_FLAT)
+                                                         : (kTex == 0 && !kMedia ? RT_WAVES_BVH_LITE : RT_WAVES_BVH))))
 void rt_render_kernel(KernelParams P) {
   extern __shared__ int smem[];
   // every wave starts with a static pool (its wave index x RT_POOL): at launch all resident waves
