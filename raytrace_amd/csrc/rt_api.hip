@@ -60,6 +60,7 @@ struct rt_device_scene {
   float* perlin_grad = nullptr;
   float* flat_recs = nullptr;
   DevBox* boxes = nullptr;
+  int leaf_exit_pct = 100;
   int* status = nullptr;
   int surface_root = RT_EMPTY_ROOT;
   int n_media = 0;
@@ -144,6 +145,7 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
     return rc;
   }
   s->surface_root = H.surface_root;
+  s->leaf_exit_pct = H.leaf_exit_pct;
   s->n_media = H.n_media;
   for (int k = 0; k < H.n_media; ++k) s->media[k] = H.media[k];
   for (int k = 0; k <= RT_MAX_MEDIA; ++k) s->flat_sets[k] = H.flat_sets[k];
@@ -202,6 +204,7 @@ int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint
   P.status = s->status;
   P.out = d_out_rgb;
   P.surface_root = s->surface_root;
+  P.leaf_exit_pct = s->leaf_exit_pct;
   P.surface_prefix = (s->variant & RT_VAR_BASE) != RT_VAR_FLAT && s->n_nodes > 0 ? 1 : 0;
   P.n_media = s->n_media;
   for (int k = 0; k < s->n_media; ++k) P.media[k] = s->media[k];

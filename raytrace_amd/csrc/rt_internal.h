@@ -198,6 +198,7 @@ struct KernelParams {
   int stack_depth;            // LDS stack entries per lane (>= the scene's BVH depth)
   int lds_nodes;              // BVH nodes [0, lds_nodes) are read from the workgroup's LDS copy
   int trav_exit_pct;          // BVH kernel: leave traversal when <= this % of live lanes trace
+  int leaf_exit_pct;          // BVH traversal: test leaves once this % of the node loop's lanes hold one
   int n_prims;                // all leaves (every set), staged in LDS by the flat kernel
   int surface_root;
   int surface_prefix;         // BVH scenes: flat_sets[0] is the surface set's prefix (rt_trace.h prefix_hits)
@@ -234,6 +235,7 @@ struct HostScene {
   bool flat = false;  // every set is a single flat leaf (no BVH nodes)
   bool noise = false;  // some texture is a noise / marble texture
   bool uv_tex = false;     // some material reads a non-constant texture (RT_VAR_TEX)
+  int leaf_exit_pct = 100;  // BVH traversal policy for this scene (KernelParams::leaf_exit_pct)
   bool full_mats = false;  // some material is not lightSource / pitchBlack / lambertian (RT_VAR_MATS)
 };
 

@@ -679,7 +679,9 @@ RT_FN void trav_round(const KernelParams& P, const RayCtx& R, TravState& S, cons
       S.node = pop();
     }
 #endif
-    if (!RT_ANY(S.leaf == 0)) break;  // every traversing lane holds a leaf
+    // leave the node loop once P.leaf_exit_pct % of its lanes hold a leaf (100: all of them,
+    // Aila & Laine's while-while); the rest keep their state and descend in the next round
+    if (RT_BALLOT_COUNT(S.leaf != 0) * 100 >= RT_BALLOT_COUNT(true) * P.leaf_exit_pct) break;
   }
   while (S.leaf < 0) {
     const int enc = ~S.leaf;

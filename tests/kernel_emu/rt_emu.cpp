@@ -109,6 +109,7 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
   P.boxes = H.boxes.data();
   P.out = out;
   P.surface_root = H.surface_root;
+  P.leaf_exit_pct = H.leaf_exit_pct;
   P.surface_prefix = H.flat ? 0 : 1;
   P.n_media = H.n_media;
   for (int k = 0; k < H.n_media; ++k) P.media[k] = H.media[k];
