@@ -61,6 +61,7 @@ struct rt_device_scene {
   float* flat_recs = nullptr;
   DevBox* boxes = nullptr;
   int leaf_exit_pct = 100;
+  int trav_exit_pct = 50;
   int* status = nullptr;
   int surface_root = RT_EMPTY_ROOT;
   int n_media = 0;
@@ -146,6 +147,7 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
   }
   s->surface_root = H.surface_root;
   s->leaf_exit_pct = H.leaf_exit_pct;
+  s->trav_exit_pct = H.trav_exit_pct;
   s->n_media = H.n_media;
   for (int k = 0; k < H.n_media; ++k) s->media[k] = H.media[k];
   for (int k = 0; k <= RT_MAX_MEDIA; ++k) s->flat_sets[k] = H.flat_sets[k];
@@ -213,6 +215,7 @@ int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint
   P.lds_nodes = s->lds_nodes;
   P.n_prims = s->n_prims;
   rt_host_plan_work(P, (long long)s->resident_blocks * rt_block_of(s->variant));
+  P.trav_exit_pct = s->trav_exit_pct;
   HIP_TRY(hipSetDevice(s->device));
   // stream-ordered workspace: fixed-point sums, NaN flags, queue counter (graph-capturable)
   const size_t tile_pixels = (size_t)P.tile_rows * P.cam.width;

@@ -693,6 +693,10 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
       spheres_only = sc->prims[order[j]].kind == RT_PRIM_SPHERE;
     S.leaf_exit_pct = spheres_only ? 100 : sc->n_media > 0 ? 60 : 30;
     if (const char* e = std::getenv("RT_AMD_LEAF_EXIT_PCT")) S.leaf_exit_pct = std::max(1, std::min(100, atoi(e)));
+    // and the decoupled lane loop's exit (KernelParams::trav_exit_pct): pawn+fog 386 -> 376 ms at
+    // 75 %, demo1 49.2 -> 48.5 at 25 %, the bunny flat between 50 and 75
+    S.trav_exit_pct = spheres_only ? 25 : sc->n_media > 0 ? 75 : 50;
+    if (const char* e = std::getenv("RT_AMD_TRAV_PCT")) S.trav_exit_pct = std::max(0, std::min(100, atoi(e)));
   }
   S.n_prims = n;
   return RT_OK;
@@ -800,8 +804,7 @@ void rt_host_plan_work(KernelParams& P, long long resident_lanes) {
   P.div_tile = rt_host_fastdiv((uint32_t)P.tile_rows * (uint32_t)P.cam.width);
   P.div_width = rt_host_fastdiv((uint32_t)P.cam.width);
   P.div_block = rt_host_fastdiv((uint32_t)P.row_block);
-  P.trav_exit_pct = 50;
-  if (const char* e = std::getenv("RT_AMD_TRAV_PCT")) P.trav_exit_pct = std::max(0, std::min(100, atoi(e)));
+  P.trav_exit_pct = 50;  // the caller sets the scene's policy (HostScene::trav_exit_pct) afterwards
   // Items = (tile pixel, chunk of consecutive samples), claimed in pixel order.  Small chunks
   // keep the 64 lanes of a wave on neighbouring pixels (coherent rays) and make the queue tail
   // short; below ~2 samples the per-item commit (3 atomics) dominates.  Measured on MI355X,

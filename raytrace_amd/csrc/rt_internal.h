@@ -236,6 +236,7 @@ struct HostScene {
   bool noise = false;  // some texture is a noise / marble texture
   bool uv_tex = false;     // some material reads a non-constant texture (RT_VAR_TEX)
   int leaf_exit_pct = 100;  // BVH traversal policy for this scene (KernelParams::leaf_exit_pct)
+  int trav_exit_pct = 50;   // and its lane-loop exit (KernelParams::trav_exit_pct)
   bool full_mats = false;  // some material is not lightSource / pitchBlack / lambertian (RT_VAR_MATS)
 };
 

@@ -117,6 +117,7 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
   P.stack_depth = H.max_depth > 1 ? H.max_depth : 1;
   P.n_prims = H.n_prims;
   rt_host_plan_work(P, 4096);
+  P.trav_exit_pct = H.trav_exit_pct;
   if (chunk > 0) {
     P.chunk = chunk;
     P.n_chunks = (P.cam.spp + chunk - 1) / chunk;
