@@ -684,14 +684,14 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   S.n_nodes = (int)(S.nodes.size() / 16);
   // BVH traversal policy (KernelParams::leaf_exit_pct), measured per scene class on MI355X:
   // testing leaves once a fifth to a third of the lanes hold one beats waiting for all of them
-  // on triangle meshes (bunny-Cornell 138 -> 113 ms at 20-30 %); with media in the queries 60 %
+  // on triangle meshes (bunny-Cornell 138 -> 113 ms at 20-30 %, 124 at 10); with media in the queries 50-60 %
   // (pawn+fog 415 -> 385 ms; 30 % is no gain there); sphere-only leaves are cheapest tested all
   // together (demo1: 100 % best, 60 % +1 %)
   {
     bool spheres_only = true;
     for (int j = (int)prefix.size(); j < n && spheres_only; ++j)
       spheres_only = sc->prims[order[j]].kind == RT_PRIM_SPHERE;
-    S.leaf_exit_pct = spheres_only ? 100 : sc->n_media > 0 ? 60 : 30;
+    S.leaf_exit_pct = spheres_only ? 100 : sc->n_media > 0 ? 55 : 25;
     if (const char* e = std::getenv("RT_AMD_LEAF_EXIT_PCT")) S.leaf_exit_pct = std::max(1, std::min(100, atoi(e)));
     // and the decoupled lane loop's exit (KernelParams::trav_exit_pct): pawn+fog 386 -> 376 ms at
     // 75 %, demo1 49.2 -> 48.5 at 25 %, the bunny flat between 50 and 75
