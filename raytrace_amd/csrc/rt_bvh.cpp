@@ -41,6 +41,7 @@ struct Builder {
   std::vector<BuildPrim>& p;
   std::vector<Node> tmp;
   int max_depth = 0;
+  int leaf_max = RT_LEAF_MAX;
   explicit Builder(std::vector<BuildPrim>& prims) : p(prims) {}
 
   Box bounds(int b, int e) const {
@@ -118,7 +119,7 @@ struct Builder {
     int mid;
     if (best_axis < 0) {
       // all centroids coincide: split in the middle of the index range
-      if (n <= RT_LEAF_MAX) {
+      if (n <= leaf_max) {
         tmp[id].first = b;
         tmp[id].count = n;
         return id;
@@ -126,7 +127,7 @@ struct Builder {
       mid = b + n / 2;
     } else {
       // SAH with traversal cost ~ 1 box pair ~ 1 primitive test
-      if (n <= RT_LEAF_MAX && leaf_cost <= node_area * 1.0 + best_cost) {
+      if (n <= leaf_max && leaf_cost <= node_area * 1.0 + best_cost) {
         tmp[id].first = b;
         tmp[id].count = n;
         return id;
@@ -153,7 +154,7 @@ inline float f_up(double x, double pad) { return std::nextafter((float)(x + pad)
 
 }  // namespace
 
-void rt_build_bvh(std::vector<BuildPrim> prims, int node_base, int prim_base, BvhOut& out) {
+void rt_build_bvh(std::vector<BuildPrim> prims, int node_base, int prim_base, BvhOut& out, int leaf_max) {
   out.nodes.clear();
   out.order.clear();
   out.n_nodes = 0;
@@ -163,6 +164,7 @@ void rt_build_bvh(std::vector<BuildPrim> prims, int node_base, int prim_base, Bv
     return;
   }
   Builder B(prims);
+  B.leaf_max = leaf_max;
   int root = B.build(0, (int)prims.size(), 0);
   out.max_depth = B.max_depth;
   for (auto& q : prims) out.order.push_back(q.index);

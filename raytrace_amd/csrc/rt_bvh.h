@@ -11,6 +11,8 @@
 
 #include <vector>
 
+#include "rt_internal.h"
+
 struct BuildPrim {
   double lo[3], hi[3];
   int index;  // caller's primitive index
@@ -26,4 +28,5 @@ struct BvhOut {
 
 // Builds a BVH over `prims`; node indices start at `node_base`, leaf primitive indices at
 // `prim_base` (the position of order[0] in the final primitive array).
-void rt_build_bvh(std::vector<BuildPrim> prims, int node_base, int prim_base, BvhOut& out);
+// leaf_max: at most this many primitives per leaf (the binned SAH decides below that)
+void rt_build_bvh(std::vector<BuildPrim> prims, int node_base, int prim_base, BvhOut& out, int leaf_max = RT_LEAF_MAX);
