@@ -26,7 +26,8 @@
 #ifndef RT_BLOCK_BVH
 #define RT_BLOCK_BVH 256      // BVH kernel workgroup (its lanes share one LDS copy of the top nodes)
 #endif
-#define RT_STACK_DEPTH 32
+#define RT_STACK_DEPTH 64     // deepest BVH accepted: the LDS stack is sized by the scene's actual depth (deep
+                              // trees lower occupancy instead of failing)
 #define RT_MAX_MEDIA 8
 #define RT_MAX_TARGETS 8
 #ifndef RT_LEAF_MAX
