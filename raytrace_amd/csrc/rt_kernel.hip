@@ -1,10 +1,11 @@
 // rt_kernel.hip — MI355X (gfx950, CDNA4) kernels: the persistent path-tracing megakernel, the
 // fixed-point resolve, and the 8-bit output epilogue.  The per-lane logic lives in rt_trace.h.
 //
-// rt_render_kernel: a grid of exactly the resident workgroups (occupancy query), 256 lanes each.
-// Lanes claim (pixel, sample-chunk) items with one wave-aggregated atomicAdd per refill
-// (ballot the lanes that need work, the lowest such lane adds popcount, the base is broadcast),
-// so consecutive lanes take consecutive pixels (coherent primary rays).  Each lane keeps its
+// rt_render_kernel: a grid of exactly the resident workgroups (occupancy query), 256 lanes each,
+// instantiated per scene class (texture level, media, materials; see render_kernel_of).  Waves
+// start with a static pool of RT_POOL item ids and refill it with one returning atomicAdd on the
+// queue head (ballot the lanes that need work; ids are handed out in lane order), so
+// consecutive lanes take consecutive pixels (coherent primary rays).  Each lane keeps its
 // BVH traversal stack in LDS, laid out [depth][lane]: the 64 lanes of a wave touch 64
 // consecutive dwords (conflict-free).  The stack depth is the scene's BVH depth (dynamic LDS),
 // so shallow scenes are not occupancy-limited by LDS.  Finished items add their int64

@@ -5,8 +5,11 @@
 // the next item from a global counter (one wave-aggregated atomic per refill), so every lane
 // stays busy until the queue drains and the tail is one chunk long.  Inside an item a lane
 // regenerates paths: when a path terminates the next sample starts at once.  Per segment:
-//   1. closest hit: the surface BVH (stack in LDS, near child first, reference depth-first
-//      tie-break) and, for every constantMedium, its boundary BVH (Geometry.hs:298-330);
+//   1. closest hit: flat sets (class loops and box groups over wave-uniform records), or the
+//      surface set's large-primitive prefix then its BVH (stack in LDS, near child first,
+//      leaves tested once a per-scene share of the lanes hold one), with the reference's
+//      depth-first tie-break in a 64-bit key; and, for every constantMedium, its boundary
+//      (Geometry.hs:298-330);
 //   2. the material of the hit: a `switch` over the ten reference materials
 //      (Material.hs:41-129) and the texture (Texture.hs:18-53);
 //   3. HemisphereF / SphereF: direction from the redirect mixture, weight pdf1 / pdf
