@@ -984,7 +984,8 @@ RT_FN bool open_item(const KernelParams& P, int item, ItemCtx& I) {
 // The lockstep persistent lane loop.  `grab(need)` is wave-collective: it returns a fresh item
 // for lanes with need == true.  `commit(tile_pixel, sx, sy, sz, bad)` adds a finished item's
 // sums.  One segment per iteration, all of its queries run by the whole wave together: the flat
-// kernel (every lane tests the same primitives) and the BVH kernel of scenes with media.
+// kernel (every lane tests the same primitives), and the lockstep BVH variant kept for
+// experiments (RT_VAR_BVH_LOCKSTEP; BVH scenes, media or not, default to lane_loop_bvh).
 template <bool kFlat, int kTex, bool kMedia, bool kMats, class Grab, class Commit>
 RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW,
                              const float* prims_) {

@@ -11,6 +11,7 @@ cp "$ROOT"/raytrace_amd/csrc/* "$W/raytrace_amd/csrc/"
 cp "$ROOT"/include/* "$W/include/"
 for r in "$@"; do cp "${r#*=}" "$W/raytrace_amd/csrc/${r%%=*}"; done
 cd "$W/raytrace_amd/csrc"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -munsafe-fp-atomics $DEFS \
-  -shared -o "$ROOT/raytrace_amd/_lib/exp/librt_amd_$NAME.so" rt_api.hip rt_kernel.hip rt_bvh.cpp rt_build.cpp
+make -s exp NAME="$NAME" DEFS="$DEFS"  # the Makefile's own flags
+mkdir -p "$ROOT/raytrace_amd/_lib/exp"
+cp "$W/raytrace_amd/_lib/exp/librt_amd_$NAME.so" "$ROOT/raytrace_amd/_lib/exp/"
 rm -rf "$W"
