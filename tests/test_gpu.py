@@ -146,6 +146,20 @@ def test_box_groups_match_oracle(gpu, oracle_mod, monkeypatch, name):
     assert pixel_agreement(a, b) >= 0.995
 
 
+@pytest.mark.parametrize("name", ["cornell", "bunny_cornell"])
+def test_item_chunk_does_not_change_the_image(gpu, monkeypatch, name):
+    """Items of 1, 3 (ragged: does not divide spp), 4 and 16 samples: a different work split
+    and commit order, the same fixed-point sums — bit-identical images."""
+    fn = {"cornell": scenes.cornell_box, "bunny_cornell": scenes.bunny_cornell}[name]
+    cs, world, seed = fn(width=64, spp=20)
+    imgs = []
+    for c in ("1", "3", "4", "16"):
+        monkeypatch.setenv("RT_AMD_CHUNK", c)
+        imgs.append(R.raytrace(cs, world, seed))
+    for img in imgs[1:]:
+        assert np.array_equal(img, imgs[0], equal_nan=True)
+
+
 def test_medium_boundary_alias_is_exact(gpu, monkeypatch):
     cs, world, seed = scenes.pawn_fog(width=96, spp=8)
     a = R.raytrace(cs, world, seed)
