@@ -22,7 +22,9 @@
 #include <string>
 #include <vector>
 
+#ifndef RT_BLOCK
 #define RT_BLOCK 256          // flat kernel workgroup
+#endif
 #ifndef RT_BLOCK_BVH
 #define RT_BLOCK_BVH 256      // BVH kernel workgroup (its lanes share one LDS copy of the top nodes)
 #endif
