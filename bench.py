@@ -11,6 +11,9 @@ ranks (one process per GPU) the frame's rows are dealt to ranks round-robin (--r
 tensor) inside the timed region — asynchronously, so frame i+1 renders while frame i's gather is in
 flight (two frame buffers); the clock stops after every frame is rendered AND gathered.
 `value` = pixels x spp of all ranks / max-over-ranks time.
+The W warm-up frames are followed by more untimed frames until the warm-up has rendered for
+--warmup-s seconds (0.5 by default; the per-frame time only settles after a few hundred ms of
+continuous rendering); `warmup_frames` / `warmup_s` in the line say how many ran.
 
 Frames of flat scenes (the Cornell box) alternate between two HIP streams (--streams 2, the
 default for them): a frame's last long paths occupy few CUs, and the next frame's persistent
@@ -121,6 +124,9 @@ def main():
                     help="frames alternate between this many HIP streams (2: frame i+1 fills the CUs that "
                          "frame i's last long paths leave idle); 0 = auto: 2 for flat scenes, 1 for BVH "
                          "scenes (two LDS-staging BVH launches interfere: bunny 20.7 -> 22.4 ms per frame)")
+    ap.add_argument("--warmup-s", type=float, default=0.5,
+                    help="after the W warm-up frames, keep warming up until the warm-up has rendered this "
+                         "many seconds (the per-frame time settles after a few hundred ms); 0: exactly W")
     ap.add_argument("--sim-shards", type=int, default=1,
                     help="diagnostic, one process: render only shard 0 of N (one rank's share of an N-GPU frame)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -206,10 +212,27 @@ def main():
         torch.cuda.synchronize(dev)
 
     # untimed warm-up: W frames, and at least one per stream (a stream's first frame pays for its
-    # stream-ordered allocation pool)
-    for _ in range(max(args.warmup, len(streams))):
-        step(False)
-    drain()
+    # stream-ordered allocation pool); then, in rounds of doubling length, until the warm-up has
+    # kept the GPU busy for --warmup-s seconds: the per-frame time settles only after a few
+    # hundred ms of continuous rendering (Cornell 3.56 ms per frame after 2 warm-up frames, 3.47
+    # after 100; one rank's share of 8: 0.577 / 0.530 ms).  Ranks agree on every round (the
+    # gathers inside the frames must match), so they all run the same number of frames.
+    k, warm_frames, warm_s = max(args.warmup, len(streams)), 0, 0.0
+    while True:
+        tw = time.perf_counter()
+        for _ in range(k):
+            step(False)
+        drain()
+        warm_s += time.perf_counter() - tw
+        warm_frames += k
+        more = warm_s < args.warmup_s and warm_frames < 100000
+        if n > 1:
+            flag = torch.tensor([int(more)], dtype=torch.int32, device=dev if args.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            more = bool(flag.item())
+        if not more:
+            break
+        k = min(2 * k, 4096)
     if n > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -271,13 +294,15 @@ def main():
         line = {
             "metric": METRIC if args.config == "cornell" else f"Msamples/s, {args.config}",
             "value": round(value, 2), "unit": "Msamples/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+            "warmup_frames": warm_frames, "warmup_s": round(warm_s, 3),
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": round(value / pub, 1) if pub else None, "dtype": "f32",
             "data": "synthetic (reference scene built in-process, no external data)",
             "config": {"workload": f"{args.config} {w}x{h} {spp}spp depth {cs.cs_maxRecursionDepth}",
                        "width": w, "height": h, "spp": spp, "max_depth": cs.cs_maxRecursionDepth,
                        "parallelism": f"rows interleaved over {n} GPU(s), row_block {args.row_block}"
-                                      + (", RCCL all_gather of the framebuffer" if n > 1 else "")},
+                                      + ((", RCCL all_gather of the framebuffer" if args.dist_backend == "nccl"
+                                          else ", gloo gather through host memory (rehearsal)") if n > 1 else "")},
             "roofline": roofline, "issue_roofline": pmc_valu(args.config, kernel_ms), "cpu_baseline": cpu,
             "check": check,
         }
