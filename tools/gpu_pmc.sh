@@ -3,7 +3,7 @@
 # usage: bash tools/gpu_pmc.sh <tag> [bench args...]
 set -o pipefail
 TAG=${1:-pmc}; shift
-ARGS=${*:-"--steps 3 --warmup 1 --no-cpu-baseline"}
+ARGS=${*:-"--steps 3 --warmup 1 --warmup-s 0 --no-cpu-baseline"}
 OUT=gpurun_out/$TAG; mkdir -p "$OUT"; export TMPDIR=/tmp
 if [ -n "$LIST" ]; then rocprofv3 -L > "$OUT/counters_list.txt" 2>&1; fi
 i=0

@@ -29,7 +29,7 @@ for s in $STEPS; do
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$OUT/pmc_$c" -o run -- \
-          python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ${CONFIG:+--config $CONFIG} > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err" || { echo "pmc $c failed"; tail -20 "$OUT/pmc_$c.err"; exit 1; }
+          python3 bench.py --steps 5 --warmup 1 --warmup-s 0 --no-cpu-baseline ${CONFIG:+--config $CONFIG} > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err" || { echo "pmc $c failed"; tail -20 "$OUT/pmc_$c.err"; exit 1; }
       done
       echo pmc done ;;
   esac
