@@ -221,7 +221,7 @@ int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint
   const size_t tile_pixels = (size_t)P.tile_rows * P.cam.width;
   const size_t off_flag = tile_pixels * 3 * sizeof(long long);
   const size_t off_ctr = off_flag + ((tile_pixels * sizeof(unsigned) + 255) & ~(size_t)255);
-  const size_t bytes = off_ctr + 256;
+  const size_t bytes = off_ctr + 256 * 8;  // up to 8 queue head words (rt_kernel.hip RT_QUEUES)
   hipStream_t st = (hipStream_t)hip_stream;
   char* ws = nullptr;
   HIP_TRY(hipMallocAsync((void**)&ws, bytes, st));

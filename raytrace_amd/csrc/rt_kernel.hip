@@ -28,32 +28,67 @@ namespace {
 #define RT_POOL 128  // 64 -> 128: Cornell 4.13 -> 4.04 ms (at 32 the head word saturates: 7.2 ms)
 #endif
 static_assert(RT_POOL >= 64, "a refill must cover every lane of a wave");
+// The dynamic ids [offset, n_items) are split into RT_QUEUES contiguous ranges, each with its own
+// head word (256 B apart): a wave starts on queue (wave % RT_QUEUES) and moves to the next one
+// when its queue is spent, so each word sees 1 / RT_QUEUES of the refills.  Measured (kernel ms,
+// 1 / 2 / 4 / 8 queues): README 0.315 / 0.282 / 0.285 / 0.29 (its cheap samples ran the single
+// word near its returning-atomic rate), README on 2 GPUs 0.191 / 0.189 / 0.177 / 0.180, Cornell
+// 3.455 / 3.42 / 3.42 / 3.43, Cornell's 8-GPU share 0.520 / 0.517 / 0.517 / 0.519.
+#ifndef RT_QUEUES
+#define RT_QUEUES 4
+#endif
+static_assert((RT_QUEUES & (RT_QUEUES - 1)) == 0 && RT_QUEUES <= 8, "RT_QUEUES: a power of two, at most 8 (workspace)");
 struct WaveGrab {
-  int* counter;
+  int* counter;  // RT_QUEUES head words, 64 ints apart
   int pool_base;
   int pool_left;
   int offset;  // ids [0, offset) are the waves' initial pools, handed out without atomics
+  int n_items;
+  int queue;  // the queue this wave refills from
+  int spent;  // queues found spent (RT_QUEUES: every id is claimed)
   __device__ __forceinline__ int operator()(bool need) {
     const unsigned long long m = __ballot(need);
     if (m == 0ull) return 0;
     const int lane = (int)__lane_id();
     const int cnt = (int)__popcll(m);
     const int rank = (int)__popcll(m & ((1ull << lane) - 1ull));
-    int item;
     if (pool_left >= cnt) {
-      item = pool_base + rank;
+      const int item = pool_base + rank;
       pool_base += cnt;
       pool_left -= cnt;
-    } else {
-      int base = 0;
-      if (lane == __ffsll((unsigned long long)m) - 1) base = atomicAdd(counter, RT_POOL);
-      base = __builtin_amdgcn_readfirstlane(__shfl(base, __ffsll((unsigned long long)m) - 1)) + offset;
-      item = rank < pool_left ? pool_base + rank : base + (rank - pool_left);
-      const int used = cnt - pool_left;
-      pool_base = base + used;
-      pool_left = RT_POOL - used;
+      return item;
     }
-    return item;
+    // ranks [0, pool_left) drain the pool; the others are served by refills, in rank order
+    int item = rank < pool_left ? pool_base + rank : n_items;
+    int first = pool_left, rest = cnt - pool_left;
+    pool_left = 0;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    const int dyn = n_items - offset;
+    const int len = dyn > 0 ? (dyn + RT_QUEUES - 1) / RT_QUEUES : 0;
+    while (rest > 0 && spent < RT_QUEUES) {
+      const int qs = offset + queue * len;
+      const int qlen = min(len, n_items - qs);  // <= 0 for an empty last queue
+      int base = 0;
+      if (lane == leader) base = atomicAdd(counter + 64 * queue, RT_POOL);
+      base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
+      if (base >= qlen) {  // spent: ids are only ever handed out below qlen
+        queue = (queue + 1) & (RT_QUEUES - 1);
+        ++spent;
+        continue;
+      }
+      const int avail = min(RT_POOL, qlen - base);
+      const int take = min(rest, avail);
+      if (rank >= first && rank < first + take) item = qs + base + (rank - first);
+      first += take;
+      rest -= take;
+      pool_base = qs + base + take;
+      pool_left = avail - take;
+      if (rest > 0) {  // the pool ended at the queue's end
+        queue = (queue + 1) & (RT_QUEUES - 1);
+        ++spent;
+      }
+    }
+    return item;  // n_items for lanes left over once every queue is spent
   }
 };
 
@@ -112,7 +147,7 @@ void rt_render_kernel(KernelParams P) {
   // would otherwise queue up on the counter at once (~80 us at ~88 returning atomics per us)
   const int waves = (int)(gridDim.x * (blockDim.x / 64));
   const int wave = (int)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
-  WaveGrab grab{P.counter, wave * RT_POOL, RT_POOL, waves * RT_POOL};
+  WaveGrab grab{P.counter, wave * RT_POOL, RT_POOL, waves * RT_POOL, P.n_items, wave & (RT_QUEUES - 1), 0};
   AtomicCommit commit{P.accum, P.nanflag};
   int overflow;
   if constexpr (kVar == RT_VAR_FLAT) {
