@@ -2,7 +2,8 @@
 //
 // Work decomposition: the frame (this shard's rows) x spp is cut into ITEMS = (tile pixel,
 // chunk of consecutive samples).  Lanes are persistent: a lane whose item is exhausted claims
-// the next item from a global counter (one wave-aggregated atomic per refill), so every lane
+// the next item from its wave's pool, refilled from one of four queue head words (one
+// wave-aggregated atomic per 128 items; rt_kernel.hip WaveGrab), so every lane
 // stays busy until the queue drains and the tail is one chunk long.  Inside an item a lane
 // regenerates paths: when a path terminates the next sample starts at once.  Per segment:
 //   1. closest hit: flat sets (class loops and box groups over wave-uniform records), or the
