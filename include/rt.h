@@ -19,11 +19,16 @@
  * The library builds its own bounding-volume hierarchy over that list; the closest hit (and
  * therefore the image) does not depend on the tree the caller wrote.
  *
- * Output.  Linear RGB, float32, row-major [row][column][rgb] — row 0 is the TOP of the image —
- * each pixel the MEAN over `samples_per_pixel` samples (Ray.hs:226-232).  Randomness is a
- * counter-based Philox4x32-10 stream keyed by `seed` and indexed by (pixel, sample, segment,
- * event), so results are deterministic for a given (scene, camera, seed) and independent of
- * the shard layout and of the GPU count.
+ * Precision.  By default the kernel computes in IEEE binary64, as the reference does (every
+ * `Vec3` is `V3 Double`, Core.hs:29-31), and writes double output.  rt_exec.flags RT_EXEC_F32
+ * selects the FP32 fast path (float output): the same algorithm, scheduling and random stream.
+ *
+ * Output.  Linear RGB, row-major [row][column][rgb] — row 0 is the TOP of the image — each
+ * pixel the MEAN over `samples_per_pixel` samples (Ray.hs:226-232); double (default) or float
+ * (RT_EXEC_F32) per channel.  Randomness is a counter-based Philox4x32-10 stream keyed by
+ * `seed` and indexed by (pixel, sample, segment, event), so results are deterministic for a
+ * given (scene, camera, seed, precision) and independent of the shard layout, of the device
+ * list and of the GPU count.
  */
 #ifndef RT_AMD_H
 #define RT_AMD_H
@@ -34,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 /* status codes */
 #define RT_OK 0
@@ -161,22 +166,38 @@ typedef struct rt_camera_settings {
   const rt_redirect_target* redirect_targets;
 } rt_camera_settings;
 
-/* Which rows this call renders.  Rows are dealt to shards in blocks of `row_block`
- * round-robin: shard r owns global rows y with (y / row_block) % n_shards == r.  With
- * n_shards > 1 every shard has the same padded row count (rt_shard_rows); padding rows are
- * written as zeros.  With n_shards == 1 the tile is exactly the image (height rows). */
+/* rt_exec.flags */
+#define RT_EXEC_F32 1          /* FP32 kernel, float output (default: binary64, double output) */
+
+#define RT_MAX_DEVICES 64
+
+/* Which rows this call renders, on which devices, in which precision.
+ *
+ * Rows are dealt to shards in blocks of `row_block` round-robin: shard r owns global rows y
+ * with (y / row_block) % n_shards == r.  With n_shards > 1 every shard has the same padded row
+ * count (rt_shard_rows); padding rows are written as zeros.  With n_shards == 1 the tile is
+ * exactly the image (height rows).  This is the one-process-per-GPU form (each rank renders
+ * its shard on `device`).
+ *
+ * Device list (rt_render only; one process, many GPUs).  With n_devices >= 1 and n_shards == 1
+ * the call renders the WHOLE image over devices[0 .. n_devices-1]: device k renders shard k of
+ * n_devices (same row interleave), all devices concurrently on their own streams, and the
+ * shard tiles are gathered into out_rgb (each device copies its tile to the host; the host
+ * un-permutes the rows).  A device may appear more than once (two shards on one GPU).  The
+ * image is bit-identical to the single-device render.  n_devices == 0: `device` alone. */
 typedef struct rt_exec {
-  int32_t device;       /* HIP device ordinal */
+  int32_t device;       /* HIP device ordinal (n_devices == 0) */
   int32_t n_shards;     /* >= 1 */
   int32_t shard;        /* 0 .. n_shards-1 */
   int32_t row_block;    /* >= 1 */
-  int32_t flags;        /* reserved, 0 */
-  int32_t pad;
+  int32_t flags;        /* RT_EXEC_* */
+  int32_t n_devices;    /* 0, or 1 .. RT_MAX_DEVICES entries of `devices` (rt_render only) */
+  const int32_t* devices;
 } rt_exec;
 
 typedef struct rt_stats {
-  double upload_ms;     /* scene build + host->device copy */
-  double kernel_ms;     /* device time of the render kernel */
+  double upload_ms;     /* scene build + host->device copy (all devices) */
+  double kernel_ms;     /* device time of the render (the slowest device of a device list) */
   double total_ms;      /* wall time of the call */
   int64_t samples;      /* pixels x spp rendered by this call */
   int32_t bvh_nodes;    /* nodes of all sets */
@@ -196,25 +217,29 @@ int rt_shard_rows(int32_t height, const rt_exec* ex);
 int rt_shard_row(int32_t t, const rt_exec* ex);
 
 /* One-shot host-buffer call — the Haskell binding's entry point (replaces Ray.hs:121-238).
- * out_rgb: caller-owned host buffer of rt_shard_rows(h, ex) * image_width * 3 floats
- * (the whole image when n_shards == 1).  Returns RT_OK or a negative RT_E_* code. */
+ * out_rgb: caller-owned host buffer of rt_shard_rows(h, ex) * image_width * 3 doubles (floats
+ * with RT_EXEC_F32); the whole image when n_shards == 1.  Returns RT_OK or a negative RT_E_*
+ * code. */
 int rt_render(const rt_camera_settings* cs, const rt_scene* scene, uint64_t seed, const rt_exec* ex,
-              float* out_rgb, rt_stats* stats);
+              void* out_rgb, rt_stats* stats);
 
 /* Device-resident path (used when inputs already live in HBM, e.g. bench.py / torch callers). */
 int rt_scene_create(const rt_scene* scene, int32_t device, rt_device_scene** out);
 int rt_scene_destroy(rt_device_scene* s);
 int rt_scene_stats(const rt_device_scene* s, rt_stats* stats);
-/* Enqueue one render on `hip_stream` (a hipStream_t, or NULL for the default stream).
- * d_out_rgb: device buffer of rt_shard_rows(h, ex) * image_width * 3 floats.  Asynchronous;
- * the scene must outlive the work. */
+/* Enqueue one render on `hip_stream` (a hipStream_t, or NULL for the default stream) of the
+ * scene's device.  d_out_rgb: device buffer of rt_shard_rows(h, ex) * image_width * 3 doubles
+ * (floats with RT_EXEC_F32).  ex->n_devices must be 0.  Asynchronous; the scene must outlive
+ * the work. */
 int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex,
-                    float* d_out_rgb, void* hip_stream);
+                    void* d_out_rgb, void* hip_stream);
 
-/* Fused output epilogue of writeImage / writeImageSqrt (Ray.hs:248-260): linear float RGB ->
- * 8-bit codes min(255, floor(256 * transfer(clamp01 x))), transfer = sRGB (encoding 0) or
- * sqrt (encoding 1).  Device pointers, asynchronous on hip_stream. */
-int rt_encode8_async(const float* d_rgb, uint8_t* d_out, int64_t n_values, int32_t encoding, void* hip_stream);
+/* Fused output epilogue of writeImage / writeImageSqrt (Ray.hs:248-260): linear RGB (float, or
+ * double with in_f64 = 1) -> 8-bit codes min(255, floor(256 * transfer(clamp01 x))), transfer =
+ * sRGB (encoding 0) or sqrt (encoding 1), evaluated in binary64; NaN -> 0.  Bit-exact against
+ * the host encoder.  Device pointers, asynchronous on hip_stream. */
+int rt_encode8_async(const void* d_rgb, int32_t in_f64, uint8_t* d_out, int64_t n_values, int32_t encoding,
+                     void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -49,9 +49,15 @@ class RtScene(ctypes.Structure):
     ]
 
 
+RT_EXEC_F32 = 1  # rt_exec.flags: FP32 kernel, float output (default: binary64, double output)
+ABI_VERSION = 3
+PRECISIONS = {"f64": np.float64, "f32": np.float32}
+
+
 class RtExec(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("n_shards", ctypes.c_int32), ("shard", ctypes.c_int32),
-                ("row_block", ctypes.c_int32), ("flags", ctypes.c_int32), ("pad", ctypes.c_int32)]
+                ("row_block", ctypes.c_int32), ("flags", ctypes.c_int32), ("n_devices", ctypes.c_int32),
+                ("devices", ctypes.POINTER(ctypes.c_int32))]
 
 
 class RtStats(ctypes.Structure):
@@ -86,10 +92,10 @@ def load():
     L.rt_scene_destroy.argtypes = [P]
     L.rt_scene_stats.argtypes = [P, ctypes.POINTER(RtStats)]
     L.rt_render_async.argtypes = [P, ctypes.POINTER(RtCameraSettings), ctypes.c_uint64, ctypes.POINTER(RtExec), P, P]
-    L.rt_encode8_async.argtypes = [P, P, ctypes.c_int64, ctypes.c_int32, P]
+    L.rt_encode8_async.argtypes = [P, ctypes.c_int32, P, ctypes.c_int64, ctypes.c_int32, P]
     for name in EXPORTED:
         getattr(L, name)
-    if L.rt_abi_version() != 2:
+    if L.rt_abi_version() != ABI_VERSION:
         raise RtDeviceError("librt_amd.so ABI version mismatch")
     _lib = L
     return L
@@ -157,7 +163,21 @@ def scene_struct(flat):
     return s
 
 
-def exec_struct(device=0, n_shards=1, shard=0, row_block=4):
+def dtype_of(precision: str):
+    """Output dtype of a precision ("f64": the reference's binary64, the default; "f32")."""
+    if precision not in PRECISIONS:
+        raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, not {precision!r}")
+    return PRECISIONS[precision]
+
+
+def exec_struct(device=0, n_shards=1, shard=0, row_block=4, precision="f64", devices=None):
+    """rt_exec: the row shard, the precision and (rt_render only) a device list."""
+    dtype_of(precision)
     e = RtExec()
-    e.device, e.n_shards, e.shard, e.row_block, e.flags = device, n_shards, shard, row_block, 0
+    e.device, e.n_shards, e.shard, e.row_block = device, n_shards, shard, row_block
+    e.flags = RT_EXEC_F32 if precision == "f32" else 0
+    if devices:
+        arr = (ctypes.c_int32 * len(devices))(*[int(d) for d in devices])
+        e.n_devices, e.devices = len(devices), ctypes.cast(arr, ctypes.POINTER(ctypes.c_int32))
+        e._keep = arr
     return e

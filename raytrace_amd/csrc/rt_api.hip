@@ -1,5 +1,6 @@
 // rt_api.hip — the C-ABI entry points of include/rt.h: scene build (rt_build.cpp), upload to
-// HBM, kernel launch (rt_kernel.hip), error reporting.
+// HBM (both precisions' records), kernel launch (rt_kernel.hip / rt_kernel64.hip), the device
+// list of rt_render (one process, many GPUs), error reporting.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -8,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -43,37 +45,128 @@ int upload(T** dst, const std::vector<T>& src) {
   return RT_OK;
 }
 
+// the device copies of one precision's records (rt_internal.h HostArraysT)
+template <class R>
+struct DevArrays {
+  R* prims = nullptr;
+  DevMaterialT<R>* prim_shade = nullptr;
+  R* prim_uv = nullptr;
+  DevMaterialT<R>* mats = nullptr;
+  DevTextureT<R>* texs = nullptr;
+  R* motions = nullptr;
+  R* uvframes = nullptr;
+  R* texels = nullptr;
+  R* perlin_grad = nullptr;
+  R* flat_recs = nullptr;
+  DevBoxT<R>* boxes = nullptr;
+  DevMediumT<R> media[RT_MAX_MEDIA];
+  int resident_blocks = 0;  // render-kernel workgroups resident on the device (occupancy query)
+  int upload(const HostArraysT<R>& H) {
+    int rc;
+    if ((rc = ::upload(&prims, H.prims)) || (rc = ::upload(&prim_shade, H.prim_shade)) ||
+        (rc = ::upload(&prim_uv, H.prim_uv)) || (rc = ::upload(&mats, H.mats)) || (rc = ::upload(&texs, H.texs)) ||
+        (rc = ::upload(&motions, H.motions)) || (rc = ::upload(&uvframes, H.uvframes)) ||
+        (rc = ::upload(&flat_recs, H.flat_recs)) || (rc = ::upload(&boxes, H.boxes)) ||
+        (rc = ::upload(&texels, H.texels)) || (rc = ::upload(&perlin_grad, H.perlin_grad)))
+      return rc;
+    for (int k = 0; k < RT_MAX_MEDIA; ++k) media[k] = H.media[k];
+    return RT_OK;
+  }
+  void release() {
+    for (void* p : {(void*)prims, (void*)prim_shade, (void*)prim_uv, (void*)mats, (void*)texs, (void*)motions,
+                    (void*)uvframes, (void*)texels, (void*)perlin_grad, (void*)flat_recs, (void*)boxes})
+      (void)hipFree(p);
+  }
+};
+
 }  // namespace
 
 struct rt_device_scene {
   int device = 0;
   float* nodes = nullptr;
-  float* prims = nullptr;
-  DevMaterial* prim_shade = nullptr;
-  float* prim_uv = nullptr;
-  DevMaterial* mats = nullptr;
-  DevTexture* texs = nullptr;
-  float* motions = nullptr;
-  float* uvframes = nullptr;
-  float* texels = nullptr;
   int* perlin_perm = nullptr;
-  float* perlin_grad = nullptr;
-  float* flat_recs = nullptr;
-  DevBox* boxes = nullptr;
+  int* status = nullptr;
+  DevArrays<float> f32;
+  DevArrays<double> f64;
   int leaf_exit_pct = 100;
   int trav_exit_pct = 50;
-  int* status = nullptr;
   int surface_root = RT_EMPTY_ROOT;
   int n_media = 0;
-  DevMedium media[RT_MAX_MEDIA];
   DevFlatSet flat_sets[1 + RT_MAX_MEDIA];
   int n_nodes = 0, n_prims = 0, max_depth = 0;
   int stack_depth = 1;       // LDS stack entries per lane
   int lds_nodes = 0;         // top surface-BVH nodes staged in LDS per workgroup
   int variant = RT_VAR_FLAT;  // render-kernel variant (rt_internal.h RT_VAR_*)
-  int resident_blocks = 0;   // render-kernel workgroups resident on the device at that stack depth
   double upload_ms = 0;
+  template <class R>
+  const DevArrays<R>& arrays() const;
 };
+template <>
+const DevArrays<float>& rt_device_scene::arrays<float>() const { return f32; }
+template <>
+const DevArrays<double>& rt_device_scene::arrays<double>() const { return f64; }
+
+namespace {
+
+// one render of the scene's records of precision R, enqueued on `stream`
+template <class R>
+int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex, R* d_out,
+                 void* hip_stream) {
+  const DevArrays<R>& A = s->arrays<R>();
+  KernelParamsT<R> P;
+  std::memset(&P, 0, sizeof P);
+  std::string err;
+  int rc = rt_host_make_params(cs, seed, ex, P, err);
+  if (rc) return fail(rc, "%s", err.c_str());
+  P.nodes = s->nodes;
+  P.prims = A.prims;
+  P.prim_shade = A.prim_shade;
+  P.prim_uv = A.prim_uv;
+  P.mats = A.mats;
+  P.texs = A.texs;
+  P.motions = A.motions;
+  P.uvframes = A.uvframes;
+  P.texels = A.texels;
+  P.perlin_perm = s->perlin_perm;
+  P.perlin_grad = A.perlin_grad;
+  P.flat_recs = A.flat_recs;
+  P.boxes = A.boxes;
+  P.status = s->status;
+  P.out = d_out;
+  P.surface_root = s->surface_root;
+  P.leaf_exit_pct = s->leaf_exit_pct;
+  P.surface_prefix = (s->variant & RT_VAR_BASE) != RT_VAR_FLAT && s->n_nodes > 0 ? 1 : 0;
+  P.n_media = s->n_media;
+  for (int k = 0; k < s->n_media; ++k) P.media[k] = A.media[k];
+  for (int k = 0; k <= RT_MAX_MEDIA; ++k) P.flat_sets[k] = s->flat_sets[k];
+  P.stack_depth = s->stack_depth;
+  P.lds_nodes = s->lds_nodes;
+  P.n_prims = s->n_prims;
+  rt_host_plan_work(P, (long long)A.resident_blocks * rt_block_of(s->variant));
+  P.trav_exit_pct = s->trav_exit_pct;
+  HIP_TRY(hipSetDevice(s->device));
+  // stream-ordered workspace: fixed-point sums, NaN flags, queue counter (graph-capturable)
+  const size_t tile_pixels = (size_t)P.tile_rows * P.cam.width;
+  const size_t off_flag = tile_pixels * RT_ACC_WORDS(R) * sizeof(long long);
+  const size_t off_ctr = off_flag + ((tile_pixels * sizeof(unsigned) + 255) & ~(size_t)255);
+  const size_t bytes = off_ctr + 256 * 8;  // up to 8 queue head words (rt_render_kernel.h RT_QUEUES)
+  hipStream_t st = (hipStream_t)hip_stream;
+  char* ws = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&ws, bytes, st));
+  HIP_TRY(hipMemsetAsync(ws, 0, bytes, st));
+  P.accum = (unsigned long long*)ws;
+  P.nanflag = (unsigned int*)(ws + off_flag);
+  P.counter = (int*)(ws + off_ctr);
+  rc = RT_OK;
+  if (rt_launch_render(P, A.resident_blocks, s->variant, hip_stream) || rt_launch_resolve(P, hip_stream))
+    rc = fail(RT_E_HIP, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+  HIP_TRY(hipFreeAsync(ws, st));
+  return rc;
+}
+
+bool exec_f32(const rt_exec* ex) { return ex && (ex->flags & RT_EXEC_F32) != 0; }
+
+}  // namespace
 
 extern "C" {
 
@@ -103,19 +196,10 @@ int rt_scene_destroy(rt_device_scene* s) {
   if (!s) return RT_OK;
   (void)hipSetDevice(s->device);
   (void)hipFree(s->nodes);
-  (void)hipFree(s->prims);
-  (void)hipFree(s->prim_shade);
-  (void)hipFree(s->prim_uv);
-  (void)hipFree(s->mats);
-  (void)hipFree(s->texs);
-  (void)hipFree(s->motions);
-  (void)hipFree(s->uvframes);
-  (void)hipFree(s->texels);
   (void)hipFree(s->perlin_perm);
-  (void)hipFree(s->perlin_grad);
-  (void)hipFree(s->flat_recs);
-  (void)hipFree(s->boxes);
   (void)hipFree(s->status);
+  s->f32.release();
+  s->f64.release();
   delete s;
   return RT_OK;
 }
@@ -135,13 +219,8 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
   auto* s = new rt_device_scene();
   s->device = device;
   std::vector<int> status(4, 0);
-  if ((rc = upload(&s->nodes, H.nodes)) || (rc = upload(&s->prims, H.prims)) ||
-      (rc = upload(&s->prim_shade, H.prim_shade)) || (rc = upload(&s->prim_uv, H.prim_uv)) ||
-      (rc = upload(&s->mats, H.mats)) || (rc = upload(&s->texs, H.texs)) || (rc = upload(&s->motions, H.motions)) ||
-      (rc = upload(&s->uvframes, H.uvframes)) || (rc = upload(&s->flat_recs, H.flat_recs)) || (rc = upload(&s->boxes, H.boxes)) ||
-      (rc = upload(&s->texels, H.texels)) || (rc = upload(&s->perlin_perm, H.perlin_perm)) ||
-      (rc = upload(&s->perlin_grad, H.perlin_grad)) ||
-      (rc = upload(&s->status, status))) {
+  if ((rc = upload(&s->nodes, H.nodes)) || (rc = upload(&s->perlin_perm, H.perlin_perm)) ||
+      (rc = upload(&s->status, status)) || (rc = s->f32.upload(H.f32)) || (rc = s->f64.upload(H.f64))) {
     rt_scene_destroy(s);
     return rc;
   }
@@ -149,7 +228,6 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
   s->leaf_exit_pct = H.leaf_exit_pct;
   s->trav_exit_pct = H.trav_exit_pct;
   s->n_media = H.n_media;
-  for (int k = 0; k < H.n_media; ++k) s->media[k] = H.media[k];
   for (int k = 0; k <= RT_MAX_MEDIA; ++k) s->flat_sets[k] = H.flat_sets[k];
   s->n_nodes = H.n_nodes;
   s->n_prims = H.n_prims;
@@ -163,8 +241,11 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
     s->lds_nodes = std::max(0, std::min(H.surface_nodes, room));
     if (const char* e = std::getenv("RT_AMD_LDS_NODES")) s->lds_nodes = std::min(s->lds_nodes, std::max(0, atoi(e)));
   }
-  s->resident_blocks = rt_render_resident_blocks(device, s->stack_depth, s->variant, s->lds_nodes);
-  if (s->resident_blocks <= 0) {
+  s->f32.resident_blocks =
+      rt_render_resident_blocks((const KernelParams*)nullptr, device, s->stack_depth, s->variant, s->lds_nodes);
+  s->f64.resident_blocks =
+      rt_render_resident_blocks((const KernelParams64*)nullptr, device, s->stack_depth, s->variant, s->lds_nodes);
+  if (s->f32.resident_blocks <= 0 || s->f64.resident_blocks <= 0) {
     rt_scene_destroy(s);
     return fail(RT_E_HIP, "occupancy query failed");
   }
@@ -183,60 +264,14 @@ int rt_scene_stats(const rt_device_scene* s, rt_stats* st) {
 }
 
 int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex,
-                    float* d_out_rgb, void* hip_stream) {
-  if (!s || !d_out_rgb) return fail(RT_E_INVALID, "null argument");
-  KernelParams P;
-  std::memset(&P, 0, sizeof P);
-  std::string err;
-  int rc = rt_host_make_params(cs, seed, ex, P, err);
-  if (rc) return fail(rc, "%s", err.c_str());
-  P.nodes = s->nodes;
-  P.prims = s->prims;
-  P.prim_shade = s->prim_shade;
-  P.prim_uv = s->prim_uv;
-  P.mats = s->mats;
-  P.texs = s->texs;
-  P.motions = s->motions;
-  P.uvframes = s->uvframes;
-  P.texels = s->texels;
-  P.perlin_perm = s->perlin_perm;
-  P.perlin_grad = s->perlin_grad;
-  P.flat_recs = s->flat_recs;
-  P.boxes = s->boxes;
-  P.status = s->status;
-  P.out = d_out_rgb;
-  P.surface_root = s->surface_root;
-  P.leaf_exit_pct = s->leaf_exit_pct;
-  P.surface_prefix = (s->variant & RT_VAR_BASE) != RT_VAR_FLAT && s->n_nodes > 0 ? 1 : 0;
-  P.n_media = s->n_media;
-  for (int k = 0; k < s->n_media; ++k) P.media[k] = s->media[k];
-  for (int k = 0; k <= RT_MAX_MEDIA; ++k) P.flat_sets[k] = s->flat_sets[k];
-  P.stack_depth = s->stack_depth;
-  P.lds_nodes = s->lds_nodes;
-  P.n_prims = s->n_prims;
-  rt_host_plan_work(P, (long long)s->resident_blocks * rt_block_of(s->variant));
-  P.trav_exit_pct = s->trav_exit_pct;
-  HIP_TRY(hipSetDevice(s->device));
-  // stream-ordered workspace: fixed-point sums, NaN flags, queue counter (graph-capturable)
-  const size_t tile_pixels = (size_t)P.tile_rows * P.cam.width;
-  const size_t off_flag = tile_pixels * 3 * sizeof(long long);
-  const size_t off_ctr = off_flag + ((tile_pixels * sizeof(unsigned) + 255) & ~(size_t)255);
-  const size_t bytes = off_ctr + 256 * 8;  // up to 8 queue head words (rt_kernel.hip RT_QUEUES)
-  hipStream_t st = (hipStream_t)hip_stream;
-  char* ws = nullptr;
-  HIP_TRY(hipMallocAsync((void**)&ws, bytes, st));
-  HIP_TRY(hipMemsetAsync(ws, 0, bytes, st));
-  P.accum = (unsigned long long*)ws;
-  P.nanflag = (unsigned int*)(ws + off_flag);
-  P.counter = (int*)(ws + off_ctr);
-  rc = RT_OK;
-  if (rt_launch_render(P, s->resident_blocks, s->variant, hip_stream) || rt_launch_resolve(P, hip_stream))
-    rc = fail(RT_E_HIP, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
-  HIP_TRY(hipFreeAsync(ws, st));
-  return rc;
+                    void* d_out_rgb, void* hip_stream) {
+  if (!s || !d_out_rgb || !ex) return fail(RT_E_INVALID, "null argument");
+  if (ex->n_devices != 0) return fail(RT_E_INVALID, "rt_render_async renders on the scene's device (n_devices = 0)");
+  if (exec_f32(ex)) return render_async<float>(s, cs, seed, ex, (float*)d_out_rgb, hip_stream);
+  return render_async<double>(s, cs, seed, ex, (double*)d_out_rgb, hip_stream);
 }
 
-int rt_render(const rt_camera_settings* cs, const rt_scene* scene, uint64_t seed, const rt_exec* ex, float* out_rgb,
+int rt_render(const rt_camera_settings* cs, const rt_scene* scene, uint64_t seed, const rt_exec* ex, void* out_rgb,
               rt_stats* stats) {
   auto t0 = std::chrono::steady_clock::now();
   if (!cs || !scene || !ex || !out_rgb) return fail(RT_E_INVALID, "null argument");
@@ -244,56 +279,132 @@ int rt_render(const rt_camera_settings* cs, const rt_scene* scene, uint64_t seed
   if (h <= 0 || cs->image_width <= 0) return fail(RT_E_INVALID, "image %dx%d must be non-empty", cs->image_width, h);
   int rows = rt_host_shard_rows(h, ex);
   if (rows < 0) return fail(RT_E_INVALID, "invalid rt_exec");
-  {  // validate the camera before touching the device
+  if (ex->n_devices < 0 || ex->n_devices > RT_MAX_DEVICES || (ex->n_devices > 0 && !ex->devices))
+    return fail(RT_E_INVALID, "invalid device list (%d devices)", ex->n_devices);
+  if (ex->n_devices > 0 && ex->n_shards != 1)
+    return fail(RT_E_INVALID, "a device list renders the whole image (n_shards must be 1)");
+  {  // validate the camera before touching a device
     KernelParams P;
     std::string err;
     int rc = rt_host_make_params(cs, seed, ex, P, err);
     if (rc) return fail(rc, "%s", err.c_str());
   }
-  rt_device_scene* s = nullptr;
-  int rc = rt_scene_create(scene, ex->device, &s);
-  if (rc) return rc;
-  size_t bytes = (size_t)rows * cs->image_width * 3 * sizeof(float);
-  float* d_out = nullptr;
-  hipStream_t st = nullptr;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  int status = 0;
-  float ms = 0;
-  if (hipMalloc((void**)&d_out, bytes ? bytes : 16) != hipSuccess) rc = fail(RT_E_HIP, "hipMalloc(%zu) failed", bytes);
-  if (!rc && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) rc = fail(RT_E_HIP, "stream create");
-  if (!rc && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) rc = fail(RT_E_HIP, "events");
-  if (!rc) {
-    (void)hipEventRecord(e0, st);
-    rc = rt_render_async(s, cs, seed, ex, d_out, st);
-    (void)hipEventRecord(e1, st);
+  const bool f32 = exec_f32(ex);
+  const size_t esize = f32 ? sizeof(float) : sizeof(double);
+  const size_t row_bytes = (size_t)cs->image_width * 3 * esize;
+  // the parts of this call: one (the rt_exec shard on `device`), or shard k of n_devices on
+  // devices[k]; each part renders into its own device buffer on its own stream, concurrently
+  const int n_parts = ex->n_devices > 0 ? ex->n_devices : 1;
+  struct Part {
+    int device = 0;
+    rt_exec ex{};
+    int rows = 0;
+    rt_device_scene* scene = nullptr;  // owned by the first part on its device
+    bool owns_scene = false;
+    void* d_out = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    std::vector<char> host;
+  };
+  std::vector<Part> parts(n_parts);
+  int rc = RT_OK;
+  for (int k = 0; k < n_parts && !rc; ++k) {
+    Part& p = parts[k];
+    p.ex = *ex;
+    p.ex.n_devices = 0;
+    p.ex.devices = nullptr;
+    if (ex->n_devices > 0) {
+      p.device = ex->devices[k];
+      p.ex.device = p.device;
+      p.ex.n_shards = n_parts;
+      p.ex.shard = k;
+    } else {
+      p.device = ex->device;
+    }
+    p.rows = rt_host_shard_rows(h, &p.ex);
+    for (int j = 0; j < k; ++j)
+      if (parts[j].device == p.device) p.scene = parts[j].scene;  // one upload per device
+    if (!p.scene) {
+      if ((rc = rt_scene_create(scene, p.device, &p.scene))) break;
+      p.owns_scene = true;
+    }
+    if (hipSetDevice(p.device) != hipSuccess) {
+      rc = fail(RT_E_HIP, "hipSetDevice(%d) failed", p.device);
+      break;
+    }
+    const size_t bytes = (size_t)p.rows * row_bytes;
+    if (hipMalloc(&p.d_out, bytes ? bytes : 16) != hipSuccess) rc = fail(RT_E_HIP, "hipMalloc(%zu) failed", bytes);
+    if (!rc && hipStreamCreateWithFlags(&p.st, hipStreamNonBlocking) != hipSuccess) rc = fail(RT_E_HIP, "stream create");
+    if (!rc && (hipEventCreate(&p.e0) != hipSuccess || hipEventCreate(&p.e1) != hipSuccess)) rc = fail(RT_E_HIP, "events");
+    if (!rc) {
+      (void)hipEventRecord(p.e0, p.st);
+      rc = rt_render_async(p.scene, cs, seed, &p.ex, p.d_out, p.st);
+      (void)hipEventRecord(p.e1, p.st);
+    }
   }
-  if (!rc && hipStreamSynchronize(st) != hipSuccess)
-    rc = fail(RT_E_HIP, "render failed: %s", hipGetErrorString(hipGetLastError()));
-  if (!rc) (void)hipEventElapsedTime(&ms, e0, e1);
-  if (!rc && hipMemcpy(out_rgb, d_out, bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(RT_E_HIP, "copy back");
-  if (!rc && hipMemcpy(&status, s->status, 4, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(RT_E_HIP, "status");
+  float ms = 0;
+  int status = 0;
+  for (int k = 0; k < n_parts && !rc; ++k) {  // every part is in flight: wait, copy back
+    Part& p = parts[k];
+    float pm = 0;
+    int ps = 0;
+    (void)hipSetDevice(p.device);
+    if (hipStreamSynchronize(p.st) != hipSuccess)
+      rc = fail(RT_E_HIP, "render on device %d failed: %s", p.device, hipGetErrorString(hipGetLastError()));
+    if (!rc) (void)hipEventElapsedTime(&pm, p.e0, p.e1);
+    ms = std::max(ms, pm);
+    const size_t bytes = (size_t)p.rows * row_bytes;
+    void* dst = out_rgb;
+    if (n_parts > 1) {
+      p.host.resize(bytes);
+      dst = p.host.data();
+    }
+    if (!rc && hipMemcpy(dst, p.d_out, bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(RT_E_HIP, "copy back");
+    if (!rc && hipMemcpy(&ps, p.scene->status, 4, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(RT_E_HIP, "status");
+    status |= ps;
+  }
   if (!rc && status) rc = fail(RT_E_STACK, "BVH traversal stack overflow");
+  if (!rc && n_parts > 1) {  // gather: shard-local row t of part k is global row rt_shard_row(t)
+    for (int k = 0; k < n_parts; ++k) {
+      const Part& p = parts[k];
+      for (int t = 0; t < p.rows; ++t) {
+        const int y = ((t / p.ex.row_block) * p.ex.n_shards + p.ex.shard) * p.ex.row_block + (t % p.ex.row_block);
+        if (y < h) std::memcpy((char*)out_rgb + (size_t)y * row_bytes, p.host.data() + (size_t)t * row_bytes, row_bytes);
+      }
+    }
+  }
   if (stats && !rc) {
     std::memset(stats, 0, sizeof *stats);
-    stats->upload_ms = s->upload_ms;
+    for (const Part& p : parts)
+      if (p.owns_scene) stats->upload_ms += p.scene->upload_ms;
     stats->kernel_ms = ms;
     stats->samples = (int64_t)rows * cs->image_width * cs->samples_per_pixel;
-    stats->bvh_nodes = s->n_nodes;
-    stats->max_stack = s->max_depth;
+    stats->bvh_nodes = parts[0].scene->n_nodes;
+    stats->max_stack = parts[0].scene->max_depth;
     stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
-  if (e0) (void)hipEventDestroy(e0);
-  if (e1) (void)hipEventDestroy(e1);
-  if (st) (void)hipStreamDestroy(st);
-  (void)hipFree(d_out);
-  rt_scene_destroy(s);
+  for (Part& p : parts) {
+    if (!p.scene) continue;
+    (void)hipSetDevice(p.device);
+    if (p.st) (void)hipStreamSynchronize(p.st);
+    if (p.e0) (void)hipEventDestroy(p.e0);
+    if (p.e1) (void)hipEventDestroy(p.e1);
+    if (p.st) (void)hipStreamDestroy(p.st);
+    (void)hipFree(p.d_out);
+  }
+  for (Part& p : parts)
+    if (p.owns_scene) rt_scene_destroy(p.scene);
   return rc;
 }
 
-int rt_encode8_async(const float* d_rgb, uint8_t* d_out, int64_t n_values, int32_t encoding, void* hip_stream) {
+int rt_encode8_async(const void* d_rgb, int32_t in_f64, uint8_t* d_out, int64_t n_values, int32_t encoding,
+                     void* hip_stream) {
   if (!d_rgb || !d_out || n_values < 0) return fail(RT_E_INVALID, "invalid encode arguments");
   if (encoding != 0 && encoding != 1) return fail(RT_E_INVALID, "encoding must be 0 (sRGB) or 1 (sqrt)");
-  if (rt_launch_encode8(d_rgb, d_out, n_values, encoding, hip_stream))
+  static double thr[2][256];
+  static std::once_flag once[2];
+  std::call_once(once[encoding], [&] { rt_host_encode8_thresholds(encoding, thr[encoding]); });
+  if (rt_launch_encode8(d_rgb, in_f64 ? 1 : 0, d_out, n_values, thr[encoding], encoding, hip_stream))
     return fail(RT_E_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
   return RT_OK;
 }

@@ -35,20 +35,32 @@ inline d3 normalize_hs(d3 v) {  // linear's normalize
   if (std::fabs(l) <= 1e-12 || std::fabs(1 - l) <= 1e-12) return v;
   return divs(v, std::sqrt(l));
 }
-inline void put3(float* dst, d3 v) {
-  dst[0] = (float)v.x;
-  dst[1] = (float)v.y;
-  dst[2] = (float)v.z;
+template <class R>
+inline void put3(R* dst, d3 v) {
+  dst[0] = (R)v.x;
+  dst[1] = (R)v.y;
+  dst[2] = (R)v.z;
 }
 inline bool finite_n(const double* p, int n) {
   for (int i = 0; i < n; ++i)
     if (!std::isfinite(p[i])) return false;
   return true;
 }
-inline float ibits(int v) {
+// an int stored in an R array: its 32-bit pattern in the low word (rt_trace.h RT_R2I)
+template <class R>
+inline R ibits(int v);
+template <>
+inline float ibits<float>(int v) {
   float f;
   std::memcpy(&f, &v, 4);
   return f;
+}
+template <>
+inline double ibits<double>(int v) {
+  const uint64_t u = (uint32_t)v;
+  double d;
+  std::memcpy(&d, &u, 8);
+  return d;
 }
 
 int fail(std::string& err, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
@@ -176,6 +188,126 @@ std::vector<BoxFound> find_boxes(const rt_scene* sc, const std::vector<int>& rec
     }
   }
   return out;
+}
+
+struct BoxCodes {
+  int ord_base, ord_code, gid_base, gid_code, prim_base, prim_code;
+};
+
+// The device records of one precision (rt_internal.h layout): primitives in `order` (slot
+// order for flat scenes, with class-grouped test copies), their materials, the textures,
+// motions, sphereUV frames, Perlin gradients and box groups.  The plane-shape frame of
+// Geometry.hs:117-131 (unit normal n, wa = v x nS, wb = nS x u, so that a = nS.((p-q) x v) =
+// (p-q).wa and b = nS.(u x (p-q)) = (p-q).wb) is computed in binary64 and rounded once to R.
+template <class R>
+void fill_records(const rt_scene* sc, const std::vector<int>& order, const std::vector<int>& slot_of, bool flat,
+                  const std::vector<BoxFound>& boxes, const std::vector<BoxCodes>& codes,
+                  const std::vector<int>& prim_mat, HostArraysT<R>& A) {
+  const int n = (int)order.size();
+  A.boxes.clear();
+  for (size_t b = 0; b < boxes.size(); ++b) {
+    DevBoxT<R> d;
+    std::memset(&d, 0, sizeof d);
+    put3(d.c, boxes[b].c);
+    put3(d.a0, boxes[b].a[0]);
+    put3(d.a1, boxes[b].a[1]);
+    put3(d.a2, boxes[b].a[2]);
+    d.ord_base = codes[b].ord_base;
+    d.ord_code = codes[b].ord_code;
+    d.gid_base = codes[b].gid_base;
+    d.gid_code = codes[b].gid_code;
+    d.prim_base = codes[b].prim_base;
+    d.prim_code = codes[b].prim_code;
+    A.boxes.push_back(d);
+  }
+  A.prims.assign((size_t)n * 16, (R)0);
+  A.prim_uv.assign((size_t)n * 6, (R)0);
+  for (int j = 0; j < n; ++j) {
+    const rt_prim& p = sc->prims[order[j]];
+    R* f = A.prims.data() + 16 * (size_t)j;
+    int kf = (p.kind == RT_PRIM_SPHERE ? 0 : p.kind == RT_PRIM_PARALLELOGRAM ? 1 : 2) |
+             (p.motion >= 0 ? RT_FLAG_MOTION : 0);
+    if (p.kind == RT_PRIM_SPHERE) {
+      f[0] = (R)p.p[0];
+      f[1] = (R)p.p[1];
+      f[2] = (R)p.p[2];
+      f[4] = (R)p.p[3];
+      f[5] = (R)(p.p[3] * p.p[3]);
+      f[6] = ibits<R>(p.uvframe);
+    } else {
+      d3 q = D3(p.p), u = D3(p.p + 3), v = D3(p.p + 6);
+      d3 cp = cross(u, v);
+      double ncp = std::sqrt(dot(cp, cp));
+      d3 nrm = divs(cp, ncp), nS = divs(nrm, ncp);
+      put3(f, nrm);
+      put3(f + 4, q);
+      put3(f + 8, cross(v, nS));
+      put3(f + 12, cross(nS, u));
+      if (!(ncp > 0)) f[0] = f[1] = f[2] = (R)0;  // the reference's normal is NaN: never hit
+      for (int k = 0; k < 6; ++k) A.prim_uv[6 * (size_t)j + k] = (R)p.uv[k];
+    }
+    f[3] = ibits<R>(kf);
+    f[7] = ibits<R>(p.gid);
+    f[11] = ibits<R>(flat ? slot_of[j] : p.order);
+    f[15] = ibits<R>(p.motion);
+  }
+  A.flat_recs.clear();
+  if (flat) {  // test order -> slot order for the shading arrays (prim index = slot)
+    A.flat_recs = A.prims;
+    std::vector<R> prims(A.prims.size()), uv(A.prim_uv.size());
+    for (int j = 0; j < n; ++j) {
+      const int k = slot_of[j];
+      std::copy(A.flat_recs.begin() + 16 * (size_t)j, A.flat_recs.begin() + 16 * (size_t)(j + 1),
+                prims.begin() + 16 * (size_t)k);
+      std::copy(A.prim_uv.begin() + 6 * (size_t)j, A.prim_uv.begin() + 6 * (size_t)(j + 1), uv.begin() + 6 * (size_t)k);
+    }
+    A.prims.swap(prims);
+    A.prim_uv.swap(uv);
+  }
+  A.mats.assign(sc->n_materials, DevMaterialT<R>{});
+  for (int i = 0; i < sc->n_materials; ++i) {
+    DevMaterialT<R>& d = A.mats[i];
+    d.kind = sc->materials[i].kind;
+    d.tex = sc->materials[i].texture;
+    d.param = (R)sc->materials[i].param;
+    const rt_texture& t = sc->textures[d.tex];
+    d.tex_const = t.kind == RT_TEX_CONSTANT ? 1 : 0;
+    for (int a = 0; a < 3; ++a) d.c0[a] = (R)t.c0[a];
+  }
+  A.prim_shade.assign(prim_mat.size(), DevMaterialT<R>{});
+  for (size_t j = 0; j < prim_mat.size(); ++j)
+    if (prim_mat[j] >= 0) A.prim_shade[j] = A.mats[prim_mat[j]];
+  A.texs.assign(sc->n_textures, DevTextureT<R>{});
+  for (int i = 0; i < sc->n_textures; ++i) {
+    const rt_texture& t = sc->textures[i];
+    DevTextureT<R>& d = A.texs[i];
+    d.kind = t.kind;
+    d.nu = t.nu;
+    d.nv = t.nv;
+    d.off = t.kind == RT_TEX_IMAGE ? t.image : 0;
+    for (int a = 0; a < 3; ++a) {
+      d.c0[a] = (R)t.c0[a];
+      d.c1[a] = (R)t.c1[a];
+    }
+    for (int a = 0; a < 8; ++a) d.prm[a] = (R)t.params[a];
+  }
+  A.texels.assign((size_t)sc->n_texels * 4, (R)0);
+  for (int i = 0; i < sc->n_texels; ++i)
+    for (int a = 0; a < 3; ++a) A.texels[4 * (size_t)i + a] = (R)sc->texels[3 * (size_t)i + a];
+  A.perlin_grad.assign(256 * 4, (R)0);
+  if (sc->perlin)
+    for (int k = 0; k < 256; ++k)
+      for (int a = 0; a < 3; ++a) A.perlin_grad[4 * k + a] = (R)sc->perlin->grad[k][a];
+  A.motions.assign((size_t)sc->n_motions * 8, (R)0);
+  for (int i = 0; i < sc->n_motions; ++i)
+    for (int a = 0; a < 3; ++a) {
+      A.motions[8 * (size_t)i + a] = (R)sc->motions[i].v0[a];
+      A.motions[8 * (size_t)i + 4 + a] = (R)sc->motions[i].v1[a];
+    }
+  A.uvframes.assign((size_t)sc->n_uvframes * 12, (R)0);
+  for (int i = 0; i < sc->n_uvframes; ++i)
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) A.uvframes[12 * (size_t)i + 4 * r + c] = (R)sc->uvframes[i].r[3 * r + c];
 }
 
 }  // namespace
@@ -539,18 +671,14 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
       }
     }
   }
+  // box groups: the faces' key orders, gids and primitive indices as base + 5-bit codes
+  std::vector<BoxCodes> box_codes;
   {
     std::vector<int> pos_of(sc->n_prims, -1);
     for (int j = 0; j < n; ++j) pos_of[order[j]] = j;
-    S.boxes.clear();
     for (size_t b = 0; b < boxes.size(); ++b) {
       const BoxFound& B = boxes[b];
-      DevBox d;
-      std::memset(&d, 0, sizeof d);
-      put3(d.c, B.c);
-      put3(d.a0, B.a[0]);
-      put3(d.a1, B.a[1]);
-      put3(d.a2, B.a[2]);
+      BoxCodes d{};
       int ord[6], gid[6], prm[6];
       int ob = INT32_MAX, gb = INT32_MAX, pb = INT32_MAX;
       for (int f = 0; f < 6; ++f) {
@@ -580,112 +708,28 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
         d.prim_code |= po << (5 * f);
       }
       if (!fits) return fail(err, RT_E_GENERIC, "box group %d: face offsets exceed the 5-bit codes", (int)b);
-      S.boxes.push_back(d);
+      box_codes.push_back(d);
     }
   }
-  S.prims.assign((size_t)n * 16, 0.0f);
   S.prim_mat.assign(n, -1);
-  S.prim_uv.assign((size_t)n * 6, 0.0f);
-  for (int j = 0; j < n; ++j) {
-    const rt_prim& p = sc->prims[order[j]];
-    float* f = S.prims.data() + 16 * (size_t)j;
-    int kf = (p.kind == RT_PRIM_SPHERE ? 0 : p.kind == RT_PRIM_PARALLELOGRAM ? 1 : 2) |
-             (p.motion >= 0 ? RT_FLAG_MOTION : 0);
-    if (p.kind == RT_PRIM_SPHERE) {
-      f[0] = (float)p.p[0];
-      f[1] = (float)p.p[1];
-      f[2] = (float)p.p[2];
-      f[4] = (float)p.p[3];
-      f[5] = (float)(p.p[3] * p.p[3]);
-      f[6] = ibits(p.uvframe);
-    } else {
-      d3 q = D3(p.p), u = D3(p.p + 3), v = D3(p.p + 6);
-      d3 cp = cross(u, v);
-      double ncp = std::sqrt(dot(cp, cp));
-      d3 nrm = divs(cp, ncp), nS = divs(nrm, ncp);
-      put3(f, nrm);
-      put3(f + 4, q);
-      put3(f + 8, cross(v, nS));
-      put3(f + 12, cross(nS, u));
-      if (!(ncp > 0)) f[0] = f[1] = f[2] = 0.0f;  // the reference's normal is NaN: never hit
-      for (int k = 0; k < 6; ++k) S.prim_uv[6 * (size_t)j + k] = (float)p.uv[k];
-    }
-    f[3] = ibits(kf);
-    f[7] = ibits(p.gid);
-    f[11] = ibits(S.flat ? slot_of[j] : p.order);
-    f[15] = ibits(p.motion);
-    S.prim_mat[j] = p.set == 0 ? p.material : -1;
-  }
-  S.flat_recs.clear();
+  for (int j = 0; j < n; ++j) S.prim_mat[j] = sc->prims[order[j]].set == 0 ? sc->prims[order[j]].material : -1;
   if (S.flat) {  // test order -> slot order for the shading arrays (prim index = slot)
-    S.flat_recs = S.prims;
-    std::vector<float> prims(S.prims.size()), uv(S.prim_uv.size());
     std::vector<int> mat(S.prim_mat.size());
-    for (int j = 0; j < n; ++j) {
-      const int k = slot_of[j];
-      std::copy(S.flat_recs.begin() + 16 * (size_t)j, S.flat_recs.begin() + 16 * (size_t)(j + 1), prims.begin() + 16 * (size_t)k);
-      std::copy(S.prim_uv.begin() + 6 * (size_t)j, S.prim_uv.begin() + 6 * (size_t)(j + 1), uv.begin() + 6 * (size_t)k);
-      mat[k] = S.prim_mat[j];
-    }
-    S.prims.swap(prims);
-    S.prim_uv.swap(uv);
+    for (int j = 0; j < n; ++j) mat[slot_of[j]] = S.prim_mat[j];
     S.prim_mat.swap(mat);
   }
-  S.mats.assign(sc->n_materials, DevMaterial{});
-  for (int i = 0; i < sc->n_materials; ++i) {
-    DevMaterial& d = S.mats[i];
-    d.kind = sc->materials[i].kind;
-    d.tex = sc->materials[i].texture;
-    d.param = (float)sc->materials[i].param;
-    const rt_texture& t = sc->textures[d.tex];
-    d.tex_const = t.kind == RT_TEX_CONSTANT ? 1 : 0;
-    for (int a = 0; a < 3; ++a) d.c0[a] = (float)t.c0[a];
-  }
-  S.prim_shade.assign(S.prim_mat.size(), DevMaterial{});
-  for (size_t j = 0; j < S.prim_mat.size(); ++j)
-    if (S.prim_mat[j] >= 0) S.prim_shade[j] = S.mats[S.prim_mat[j]];
-  S.texs.assign(sc->n_textures, DevTexture{});
-  for (int i = 0; i < sc->n_textures; ++i) {
-    const rt_texture& t = sc->textures[i];
-    DevTexture& d = S.texs[i];
-    d.kind = t.kind;
-    d.nu = t.nu;
-    d.nv = t.nv;
-    d.off = t.kind == RT_TEX_IMAGE ? t.image : 0;
-    for (int a = 0; a < 3; ++a) {
-      d.c0[a] = (float)t.c0[a];
-      d.c1[a] = (float)t.c1[a];
-    }
-    for (int a = 0; a < 8; ++a) d.prm[a] = (float)t.params[a];
-  }
-  S.texels.assign((size_t)sc->n_texels * 4, 0.0f);
-  for (int i = 0; i < sc->n_texels; ++i)
-    for (int a = 0; a < 3; ++a) S.texels[4 * (size_t)i + a] = sc->texels[3 * (size_t)i + a];
+  fill_records(sc, order, slot_of, S.flat, boxes, box_codes, S.prim_mat, S.f32);
+  fill_records(sc, order, slot_of, S.flat, boxes, box_codes, S.prim_mat, S.f64);
+  S.n_boxes = (int)boxes.size();
   S.perlin_perm.assign(3 * 256, 0);
-  S.perlin_grad.assign(256 * 4, 0.0f);
-  if (sc->perlin) {
+  if (sc->perlin)
     for (int a = 0; a < 3; ++a)
       for (int k = 0; k < 256; ++k) S.perlin_perm[256 * a + k] = sc->perlin->perm[a][k];
-    for (int k = 0; k < 256; ++k)
-      for (int a = 0; a < 3; ++a) S.perlin_grad[4 * k + a] = (float)sc->perlin->grad[k][a];
-  }
-  S.motions.assign((size_t)sc->n_motions * 8, 0.0f);
-  for (int i = 0; i < sc->n_motions; ++i)
-    for (int a = 0; a < 3; ++a) {
-      S.motions[8 * (size_t)i + a] = (float)sc->motions[i].v0[a];
-      S.motions[8 * (size_t)i + 4 + a] = (float)sc->motions[i].v1[a];
-    }
-  S.uvframes.assign((size_t)sc->n_uvframes * 12, 0.0f);
-  for (int i = 0; i < sc->n_uvframes; ++i)
-    for (int r = 0; r < 3; ++r)
-      for (int c = 0; c < 3; ++c) S.uvframes[12 * (size_t)i + 4 * r + c] = (float)sc->uvframes[i].r[3 * r + c];
   S.surface_root = roots[0];
   S.n_media = sc->n_media;
   for (int k = 0; k < sc->n_media; ++k) {
-    S.media[k].neg_inv_density = (float)(-(1.0 / sc->media[k].density));
-    S.media[k].material = sc->media[k].material;
-    S.media[k].root = roots[k + 1];
-    S.media[k].alias_surface = alias[k];
+    S.f32.media[k] = DevMedium{(float)(-(1.0 / sc->media[k].density)), sc->media[k].material, roots[k + 1], alias[k]};
+    S.f64.media[k] = DevMediumT<double>{-(1.0 / sc->media[k].density), sc->media[k].material, roots[k + 1], alias[k]};
   }
   S.n_nodes = (int)(S.nodes.size() / 16);
   // BVH traversal policy (KernelParams::leaf_exit_pct), measured per scene class on MI355X:
@@ -719,7 +763,8 @@ int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex) {
          (tex ? RT_VAR_TEX : 0);
 }
 
-int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex, KernelParams& P,
+template <class R>
+int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex, KernelParamsT<R>& P,
                         std::string& err) {
   if (!cs || !ex) return fail(err, RT_E_INVALID, "null argument");
   if (cs->image_width <= 0) return fail(err, RT_E_INVALID, "image width must be positive");
@@ -737,7 +782,7 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
     return fail(err, RT_E_INVALID, "non-finite camera settings");
   int rows = rt_host_shard_rows(h, ex);
   if (rows < 0) return fail(err, RT_E_INVALID, "invalid rt_exec");
-  // Ray.hs:122-136, 153-155 in binary64, rounded once to FP32
+  // Ray.hs:122-136, 153-155 in binary64, rounded once to R
   d3 center = D3(cs->center), look = D3(cs->look_at), up = D3(cs->up);
   double vh = cs->focus_dist * std::tan(cs->vfov / 2) * 2;
   double vw = vh * (double)cs->image_width / (double)h;
@@ -768,7 +813,7 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
   std::memset(P.targets, 0, sizeof P.targets);
   for (int k = 0; k < cs->n_redirect_targets; ++k) {
     const rt_redirect_target& t = cs->redirect_targets[k];
-    DevTarget& T = P.targets[k];
+    DevTargetT<R>& T = P.targets[k];
     d3 q = D3(t.q), uu = D3(t.u), vv = D3(t.v);
     d3 cp = cross(uu, vv);
     double ncp = std::sqrt(dot(cp, cp));
@@ -783,10 +828,10 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
     put3(T.cr, cp);
     cum = (k == 0) ? t.prob : cum + t.prob;
     psum = (k == 0) ? t.prob : psum + t.prob;
-    T.prob = (float)t.prob;
-    T.thresh = (float)cum;
+    T.prob = (R)t.prob;
+    T.thresh = (R)cum;
   }
-  P.rem_prob = (float)(1.0 - psum);
+  P.rem_prob = (R)(1.0 - psum);
   P.key0 = (uint32_t)seed;
   P.key1 = (uint32_t)(seed >> 32);
   P.n_shards = ex->n_shards;
@@ -806,7 +851,8 @@ FastDiv rt_host_fastdiv(uint32_t d) {
   return f;
 }
 
-void rt_host_plan_work(KernelParams& P, long long resident_lanes) {
+template <class R>
+void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes) {
   P.div_tile = rt_host_fastdiv((uint32_t)P.tile_rows * (uint32_t)P.cam.width);
   P.div_width = rt_host_fastdiv((uint32_t)P.cam.width);
   P.div_block = rt_host_fastdiv((uint32_t)P.row_block);
@@ -837,4 +883,45 @@ void rt_host_plan_work(KernelParams& P, long long resident_lanes) {
   P.chunk = chunk;
   P.n_chunks = (spp + chunk - 1) / chunk;
   P.n_items = (int)items;
+}
+
+template int rt_host_make_params<float>(const rt_camera_settings*, uint64_t, const rt_exec*, KernelParamsT<float>&,
+                                        std::string&);
+template int rt_host_make_params<double>(const rt_camera_settings*, uint64_t, const rt_exec*, KernelParamsT<double>&,
+                                         std::string&);
+template void rt_host_plan_work<float>(KernelParamsT<float>&, long long);
+template void rt_host_plan_work<double>(KernelParamsT<double>&, long long);
+
+// The 8-bit code of writeImage / writeImageSqrt's quantisation, exactly as the host encoder
+// computes it (raytrace_amd.ray.encode8: binary64, libm pow / sqrt).
+static int encode8_code(double x, int encoding) {
+  x = std::isnan(x) ? 0.0 : std::min(1.0, std::max(0.0, x));
+  const double t = encoding == 1 ? std::sqrt(x) : (x <= 0.0031308 ? 12.92 * x : 1.055 * std::pow(x, 1 / 2.4) - 0.055);
+  const double c = std::floor(256.0 * t);
+  return c > 255.0 ? 255 : (int)c;
+}
+
+void rt_host_encode8_thresholds(int encoding, double* thr) {
+  // the code is monotone in x; binary search over the ordered bit patterns of [0, 1]
+  thr[0] = 0.0;
+  for (int k = 1; k < 256; ++k) {
+    uint64_t lo = 0, hi = 0x3FF0000000000000ull;  // code(lo) < k <= code(hi) (code(1) = 255)
+    auto at = [](uint64_t b) {
+      double d;
+      std::memcpy(&d, &b, 8);
+      return d;
+    };
+    if (encode8_code(0.0, encoding) >= k) {
+      thr[k] = 0.0;
+      continue;
+    }
+    while (hi - lo > 1) {
+      const uint64_t mid = lo + (hi - lo) / 2;
+      if (encode8_code(at(mid), encoding) >= k)
+        hi = mid;
+      else
+        lo = mid;
+    }
+    thr[k] = at(hi);
+  }
 }

@@ -73,28 +73,38 @@ int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex);
 #define RT_EV_SCATTER 2u
 #define RT_EV_MEDIA 3u
 
-// Material record (32 B).  A constant texture's colour is folded in (tex_const = 1), so the
+// Precision.  The reference computes in binary64 (`V3 Double`, Core.hs:29-31); the kernel is
+// compiled for R = double (the default: rt_exec.flags without RT_EXEC_F32) and for R = float
+// (the opt-in fast path).  Every record that holds scene values is a template over R; BVH
+// nodes stay float in both (their boxes are rounded outward and padded, rt_bvh.cpp, so they
+// are conservative for the binary64 primitives too).  Integer fields stored inside an R array
+// (kind, gid, order, motion) keep their 32-bit pattern in the low word: rt_trace.h RT_R2I.
+
+// Material record (32 B for float).  A constant texture's colour is folded in (tex_const = 1), so the
 // common case needs no texture-table read; prim_shade holds one copy per primitive, so a surface
 // hit reaches its material in one load (not primitive -> material index -> material -> texture).
-struct DevMaterial {
+template <class R>
+struct DevMaterialT {
   int kind;
   int tex;
-  float param;
+  R param;
   int tex_const;
-  float c0[3];
-  float pad;
+  R c0[3];
+  R pad;
 };
 
-struct DevTexture {
+template <class R>
+struct DevTextureT {
   int kind, nu, nv, off;  // RT_TEX_*; checker dims | image width, height, first texel | noise layers
-  float c0[3];
-  float c1[3];
-  float prm[8];           // noise: freq, shift.xyz | marble: dir.xyz, freq, shift.xyz
-  float pad[2];
+  R c0[3];
+  R c1[3];
+  R prm[8];               // noise: freq, shift.xyz | marble: dir.xyz, freq, shift.xyz
+  R pad[2];
 };
 
-struct DevMedium {
-  float neg_inv_density;  // -(1 / density)  (Geometry.hs:303)
+template <class R>
+struct DevMediumT {
+  R neg_inv_density;      // -(1 / density)  (Geometry.hs:303)
   int material;
   int root;               // BVH root of the boundary set
   int alias_surface;      // 1: the boundary set is geometrically the surface set (see below)
@@ -110,7 +120,7 @@ struct DevMedium {
 // one specialised, branch-free loop per class: [first, end_quad) static parallelograms,
 // [end_quad, end_tri) static triangles, [end_tri, end_sphere) static spheres,
 // [end_sphere, end) moving primitives of any kind.  Each record's order word holds its SLOT:
-// set first + rank of its depth-first `order` within the set, so the 64-bit closest-hit key
+// set first + rank of its depth-first `order` within the set, so the closest-hit key
 // (t, slot) keeps the reference's tie-break whatever the test order, and the winner's index is
 // its slot: flat scenes store `prims` in slot order and test class-grouped copies (flat_recs), so
 // the loop tracks only the key and the winner's primitive index IS its slot.
@@ -131,36 +141,39 @@ struct DevFlatSet {
 // f = 2 * axis + side (side 1 = the s_axis = 1 end); each face's key order, gid and primitive
 // are base + a 5-bit offset packed at bit 5 f of the codes (31: the box has no such face).
 // The face primitives stay in the primitive array (shading reads them) after the set's tested
-// range.  The closest hit is the reference's up to FP32 rounding at the boxes' edges.
+// range.  The closest hit is the reference's up to rounding at the boxes' edges.
 #define RT_BOX_NO_FACE 31
-struct DevBox {
-  float c[3];      // corner (s = 0 on every axis)
+template <class R>
+struct DevBoxT {
+  R c[3];          // corner (s = 0 on every axis)
   int ord_base;    // key order (flat: slot; prefix: depth-first order) of the faces
-  float a0[3];     // axis_0 / L_0: s_0 = a0 . (p - c) in [0, 1] inside
+  R a0[3];         // axis_0 / L_0: s_0 = a0 . (p - c) in [0, 1] inside
   int ord_code;
-  float a1[3];
+  R a1[3];
   int gid_base;
-  float a2[3];
+  R a2[3];
   int gid_code;
   int prim_base;   // primitive index of the faces
   int prim_code;
   int pad[2];
 };
 
-struct DevTarget {
-  float q[3], u[3], v[3];
-  float n[3];     // unit normal of u x v
-  float wa[3];    // v x nS
-  float wb[3];    // nS x u
-  float cr[3];    // u x v (pdf denominator, Ray.hs:202)
-  float prob;
-  float thresh;   // cumulative probability (scanl1 (+) probs)
-  float pad;
+template <class R>
+struct DevTargetT {
+  R q[3], u[3], v[3];
+  R n[3];     // unit normal of u x v
+  R wa[3];    // v x nS
+  R wb[3];    // nS x u
+  R cr[3];    // u x v (pdf denominator, Ray.hs:202)
+  R prob;
+  R thresh;   // cumulative probability (scanl1 (+) probs)
+  R pad;
 };
 
-struct DevCamera {
-  float center[3], top_left[3], pixel_u[3], pixel_v[3], disk_u[3], disk_v[3];
-  float bg0[3], bg1[3];
+template <class R>
+struct DevCameraT {
+  R center[3], top_left[3], pixel_u[3], pixel_v[3], disk_u[3], disk_v[3];
+  R bg0[3], bg1[3];
   int width, height, spp, max_depth, bg_kind;
   int pad;
 };
@@ -175,24 +188,25 @@ struct FastDiv {
   int pad;
 };
 
-struct KernelParams {
-  const float* nodes;      // 16 floats per node
-  const float* prims;      // 16 floats per primitive
-  const DevMaterial* prim_shade;  // per primitive: its material record (DevMaterial)
-  const float* prim_uv;    // 6 floats per primitive
-  const DevMaterial* mats;
-  const DevTexture* texs;
-  const float* motions;    // 8 floats per motion: v0.xyz, -, v1.xyz, -
-  const float* uvframes;   // 12 floats per frame: rows of R (xyz, -)
-  const float* texels;     // image textures: 4 floats per texel (linear RGB, -)
+template <class R>
+struct KernelParamsT {
+  const float* nodes;      // 16 floats per node (both precisions)
+  const R* prims;          // 16 R per primitive
+  const DevMaterialT<R>* prim_shade;  // per primitive: its material record (DevMaterial)
+  const R* prim_uv;        // 6 R per primitive
+  const DevMaterialT<R>* mats;
+  const DevTextureT<R>* texs;
+  const R* motions;        // 8 R per motion: v0.xyz, -, v1.xyz, -
+  const R* uvframes;       // 12 R per frame: rows of R (xyz, -)
+  const R* texels;         // image textures: 4 R per texel (linear RGB, -)
   const int* perlin_perm;  // 3 x 256 permutation entries (Noise.hs permX / permY / permZ)
-  const float* perlin_grad;  // 256 gradients, 4 floats each (xyz, -)
-  const float* flat_recs;  // flat scenes: the test records, class-grouped (DevFlatSet ranges)
-  const DevBox* boxes;     // box groups of the flat sets / the surface prefix (DevBox)
-  float* out;
+  const R* perlin_grad;    // 256 gradients, 4 R each (xyz, -)
+  const R* flat_recs;      // flat scenes: the test records, class-grouped (DevFlatSet ranges)
+  const DevBoxT<R>* boxes; // box groups of the flat sets / the surface prefix (DevBox)
+  R* out;                  // linear RGB of the tile, R per channel
   int* status;             // device word: nonzero on stack overflow
   // persistent-lane work queue (rt_trace.h lane_loop): items = n_chunks x tile pixels
-  unsigned long long* accum;  // 3 x int64 fixed-point (2^-32) radiance sums per tile pixel
+  unsigned long long* accum;  // fixed-point radiance sums per tile pixel: RT_ACC_WORDS(R) x int64
   unsigned int* nanflag;      // per tile pixel: a sample produced a non-finite radiance
   int* counter;               // next unclaimed item
   int chunk;                  // samples per item
@@ -202,38 +216,56 @@ struct KernelParams {
   int lds_nodes;              // BVH nodes [0, lds_nodes) are read from the workgroup's LDS copy
   int trav_exit_pct;          // BVH kernel: leave traversal when <= this % of live lanes trace
   int leaf_exit_pct;          // BVH traversal: test leaves once this % of the node loop's lanes hold one
-  int n_prims;                // all leaves (every set), staged in LDS by the flat kernel
+  int n_prims;                // all leaves (every set)
   int surface_root;
   int surface_prefix;         // BVH scenes: flat_sets[0] is the surface set's prefix (rt_trace.h prefix_hits)
   int n_media;
   int n_targets;
-  float rem_prob;
-  DevMedium media[RT_MAX_MEDIA];
+  R rem_prob;
+  DevMediumT<R> media[RT_MAX_MEDIA];
   DevFlatSet flat_sets[1 + RT_MAX_MEDIA];  // flat kernel: set 0 = surfaces, set m + 1 = medium m
-  DevTarget targets[RT_MAX_TARGETS];
-  DevCamera cam;
+  DevTargetT<R> targets[RT_MAX_TARGETS];
+  DevCameraT<R> cam;
   uint32_t key0, key1;
   int n_shards, shard, row_block, tile_rows;
   FastDiv div_tile, div_width, div_block;  // tile pixels, image width, row block
 };
+using DevMaterial = DevMaterialT<float>;
+using DevTexture = DevTextureT<float>;
+using DevMedium = DevMediumT<float>;
+using DevBox = DevBoxT<float>;
+using DevTarget = DevTargetT<float>;
+using DevCamera = DevCameraT<float>;
+using KernelParams = KernelParamsT<float>;
+using KernelParams64 = KernelParamsT<double>;
 
 #define RT_FIX_SCALE 4294967296.0  // 2^32: per-sample radiance is accumulated as int64 * 2^-32
+// Fixed-point words per pixel: float kernels add trunc(x 2^32) per channel (3 words); binary64
+// kernels add trunc(x 2^32) and the next 32 bits of x 2^64 as a second word per channel (6
+// words: x to 2^-64, every bit of a binary64 radiance >= 2^-11).  Integer sums commute, so the
+// mean is bit-for-bit independent of the schedule and of the shard layout in both precisions.
+#define RT_ACC_WORDS(R) (sizeof(R) == 8 ? 6 : 3)
 
-// Host-side scene image, ready for upload (rt_build.cpp).
+// Host-side scene image, ready for upload (rt_build.cpp): the records of one precision
+template <class R>
+struct HostArraysT {
+  std::vector<R> prims, prim_uv, motions, uvframes, texels, perlin_grad;
+  std::vector<R> flat_recs;  // flat scenes: class-grouped copies of the records (prims is in slot order)
+  std::vector<DevMaterialT<R>> prim_shade, mats;
+  std::vector<DevTextureT<R>> texs;
+  std::vector<DevBoxT<R>> boxes;  // box groups (DevBox)
+  DevMediumT<R> media[RT_MAX_MEDIA];
+};
 struct HostScene {
-  std::vector<float> nodes, prims, prim_uv, motions, uvframes, texels, perlin_grad;
+  std::vector<float> nodes;  // BVH nodes (float in both precisions)
   std::vector<int> perlin_perm;
   std::vector<int> prim_mat;        // material index per primitive (-1: medium boundary)
-  std::vector<DevMaterial> prim_shade;
-  std::vector<float> flat_recs;  // flat scenes: class-grouped copies of the records (prims is in slot order)
-  std::vector<DevBox> boxes;   // box groups (DevBox)
-  std::vector<DevMaterial> mats;
-  std::vector<DevTexture> texs;
+  HostArraysT<float> f32;           // records of the float kernels
+  HostArraysT<double> f64;          // records of the binary64 kernels
   int surface_root = RT_EMPTY_ROOT;
   int n_media = 0;
-  DevMedium media[RT_MAX_MEDIA];
   DevFlatSet flat_sets[1 + RT_MAX_MEDIA] = {};
-  int n_nodes = 0, n_prims = 0, max_depth = 0;
+  int n_nodes = 0, n_prims = 0, max_depth = 0, n_boxes = 0;
   int surface_nodes = 0;  // nodes of the surface BVH: [0, surface_nodes), breadth-first
   bool flat = false;  // every set is a single flat leaf (no BVH nodes)
   bool noise = false;  // some texture is a noise / marble texture
@@ -241,7 +273,13 @@ struct HostScene {
   int leaf_exit_pct = 100;  // BVH traversal policy for this scene (KernelParams::leaf_exit_pct)
   int trav_exit_pct = 50;   // and its lane-loop exit (KernelParams::trav_exit_pct)
   bool full_mats = false;  // some material is not lightSource / pitchBlack / lambertian (RT_VAR_MATS)
+  template <class R>
+  const HostArraysT<R>& arrays() const;
 };
+template <>
+inline const HostArraysT<float>& HostScene::arrays<float>() const { return f32; }
+template <>
+inline const HostArraysT<double>& HostScene::arrays<double>() const { return f64; }
 
 struct rt_scene;
 struct rt_camera_settings;
@@ -251,18 +289,27 @@ struct rt_exec;
 int rt_host_build_scene(const rt_scene* sc, HostScene& out, std::string& err);
 int rt_host_image_height(const rt_camera_settings* cs);
 int rt_host_shard_rows(int height, const rt_exec* ex);
-// fills camera / targets / tiling / key of P (pointers are left to the caller)
-int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex, KernelParams& P,
+// fills camera / targets / tiling / key of P (pointers are left to the caller); R = float, double
+template <class R>
+int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex, KernelParamsT<R>& P,
                         std::string& err);
+// work decomposition (rt_build.cpp): chunk so that items >= ~8 x resident lanes
+template <class R>
+void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes);
+FastDiv rt_host_fastdiv(uint32_t d);
+// the 8-bit code thresholds of the output epilogue (rt_build.cpp): thr[k] = the smallest binary64
+// x in [0, 1] whose code min(255, floor(256 transfer(x))) is >= k (k = 1..255; thr[0] = 0)
+void rt_host_encode8_thresholds(int encoding, double* thr);
 
-// rt_kernel.hip (device launchers)
+// rt_kernel.hip / rt_kernel64.hip (device launchers)
 // resident workgroups of the render kernel for a given LDS stack depth (occupancy query)
-// flat: the variant for scenes whose sets are all single flat leaves (prims staged in LDS)
-int rt_render_resident_blocks(int device, int stack_depth, int variant, int lds_nodes);
+int rt_render_resident_blocks(const KernelParams*, int device, int stack_depth, int variant, int lds_nodes);
+int rt_render_resident_blocks(const KernelParams64*, int device, int stack_depth, int variant, int lds_nodes);
 int rt_launch_render(const KernelParams& p, int grid_blocks, int variant, void* stream);
+int rt_launch_render(const KernelParams64& p, int grid_blocks, int variant, void* stream);
 // accum / nanflag -> out (mean over spp, NaN where flagged)
 int rt_launch_resolve(const KernelParams& p, void* stream);
-// work decomposition (rt_build.cpp): chunk so that items >= ~8 x resident lanes
-void rt_host_plan_work(KernelParams& P, long long resident_lanes);
-FastDiv rt_host_fastdiv(uint32_t d);
-int rt_launch_encode8(const float* in, uint8_t* out, int64_t n, int encoding, void* stream);
+int rt_launch_resolve(const KernelParams64& p, void* stream);
+// 8-bit epilogue over float (in_f64 = 0) or binary64 (1) values; thr: 256 host thresholds
+int rt_launch_encode8(const void* in, int in_f64, uint8_t* out, int64_t n, const double* thr, int encoding,
+                      void* stream);

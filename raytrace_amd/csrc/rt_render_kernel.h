@@ -1,0 +1,276 @@
+// rt_render_kernel.h — the persistent path-tracing megakernel, the fixed-point resolve and
+// their launchers for ONE precision: included by rt_kernel.hip (RT_F64 0, float) and
+// rt_kernel64.hip (RT_F64 1, binary64), each its own translation unit (built in parallel).
+// The per-lane logic lives in rt_trace.h.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rt_trace.h"
+
+namespace RT_NS {
+namespace {
+
+// Item claims.  A wave keeps a pool of consecutive item ids in SGPRs (wave-uniform state) and
+// refills it with ONE returning atomicAdd of RT_POOL ids, so the global head word sees one
+// atomic per RT_POOL claims instead of one per refilling wave-iteration (a single word saturates at
+// ~88 returning atomics per microsecond, MI355X_MICROARCH.md "dequeue").  Lanes that need work
+// take ids in lane order; ids are never dropped (a pool is contiguous and increasing, so once a
+// lane draws an id >= n_items every later id is out of range too).
+#ifndef RT_POOL
+#define RT_POOL 128  // 64 -> 128: Cornell 4.13 -> 4.04 ms (at 32 the head word saturates: 7.2 ms)
+#endif
+static_assert(RT_POOL >= 64, "a refill must cover every lane of a wave");
+// The dynamic ids [offset, n_items) are split into RT_QUEUES contiguous ranges, each with its own
+// head word (256 B apart): a wave starts on queue (wave % RT_QUEUES) and moves to the next one
+// when its queue is spent, so each word sees 1 / RT_QUEUES of the refills.  Measured (kernel ms,
+// 1 / 2 / 4 / 8 queues): README 0.315 / 0.282 / 0.285 / 0.29 (its cheap samples ran the single
+// word near its returning-atomic rate), README on 2 GPUs 0.191 / 0.189 / 0.177 / 0.180, Cornell
+// 3.455 / 3.42 / 3.42 / 3.43, Cornell's 8-GPU share 0.520 / 0.517 / 0.517 / 0.519.
+#ifndef RT_QUEUES
+#define RT_QUEUES 4
+#endif
+static_assert((RT_QUEUES & (RT_QUEUES - 1)) == 0 && RT_QUEUES <= 8, "RT_QUEUES: a power of two, at most 8 (workspace)");
+struct WaveGrab {
+  int* counter;  // RT_QUEUES head words, 64 ints apart
+  int pool_base;
+  int pool_left;
+  int offset;  // ids [0, offset) are the waves' initial pools, handed out without atomics
+  int n_items;
+  int queue;  // the queue this wave refills from
+  int spent;  // queues found spent (RT_QUEUES: every id is claimed)
+  __device__ __forceinline__ int operator()(bool need) {
+    const unsigned long long m = __ballot(need);
+    if (m == 0ull) return 0;
+    const int lane = (int)__lane_id();
+    const int cnt = (int)__popcll(m);
+    const int rank = (int)__popcll(m & ((1ull << lane) - 1ull));
+    if (pool_left >= cnt) {
+      const int item = pool_base + rank;
+      pool_base += cnt;
+      pool_left -= cnt;
+      return item;
+    }
+    // ranks [0, pool_left) drain the pool; the others are served by refills, in rank order
+    int item = rank < pool_left ? pool_base + rank : n_items;
+    int first = pool_left, rest = cnt - pool_left;
+    pool_left = 0;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    const int dyn = n_items - offset;
+    const int len = dyn > 0 ? (dyn + RT_QUEUES - 1) / RT_QUEUES : 0;
+    while (rest > 0 && spent < RT_QUEUES) {
+      const int qs = offset + queue * len;
+      const int qlen = min(len, n_items - qs);  // <= 0 for an empty last queue
+      int base = 0;
+      if (lane == leader) base = atomicAdd(counter + 64 * queue, RT_POOL);
+      base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
+      if (base >= qlen) {  // spent: ids are only ever handed out below qlen
+        queue = (queue + 1) & (RT_QUEUES - 1);
+        ++spent;
+        continue;
+      }
+      const int avail = min(RT_POOL, qlen - base);
+      const int take = min(rest, avail);
+      if (rank >= first && rank < first + take) item = qs + base + (rank - first);
+      first += take;
+      rest -= take;
+      pool_base = qs + base + take;
+      pool_left = avail - take;
+      if (rest > 0) {  // the pool ended at the queue's end
+        queue = (queue + 1) & (RT_QUEUES - 1);
+        ++spent;
+      }
+    }
+    return item;  // n_items for lanes left over once every queue is spent
+  }
+};
+
+// A finished item's fixed-point sums (rt_trace.h Acc): RT_ACC_WORDS 64-bit integer atomics per
+// pixel, [hi.xyz] (float) or [hi.xyz, lo.xyz] (binary64); zero words are skipped.
+struct AtomicCommit {
+  unsigned long long* accum;
+  unsigned int* nanflag;
+  __device__ __forceinline__ void operator()(int tp, const Acc& A, bool bad) const {
+#ifdef RT_EXP_NO_COMMIT  // ablation: drop the sums (wrong image), measures the cost of the atomics
+    if (A.hi[0] != 12345) return;
+#endif
+    unsigned long long* a = accum + RT_ACC_WORDS(real) * (size_t)tp;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      if (A.hi[c]) atomicAdd(a + c, (unsigned long long)A.hi[c]);
+#if RT_F64
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      if (A.lo[c]) atomicAdd(a + 3 + c, A.lo[c]);
+#endif
+    if (bad) atomicOr(nanflag + tp, 1u);
+  }
+};
+
+}  // namespace
+
+// Variants (rt_internal.h RT_VAR_*), chosen per scene by the host:
+//  RT_VAR_FLAT: every primitive set is one flat leaf; no LDS: the records are read with
+//    wave-uniform addresses (scalar loads into SGPRs, scalar-cache resident); lockstep loop.
+//  RT_VAR_BVH / RT_VAR_BVH_LOCKSTEP: BVH scenes; dynamic LDS = the lanes' traversal stacks
+//    [depth][lane] followed by the top P.lds_nodes nodes.  The default decouples traversal
+//    from shading per lane (rt_trace.h lane_loop_bvh); the lockstep loop runs every query of a
+//    segment with the whole wave (kept for experiments; images are bit-identical).
+// Register budget: occupancy floor (waves per SIMD).  Flat: 7 (72 VGPRs, no spills; 2.8%
+// faster on the Cornell box than the 6 it fits unforced, 8 spills and is slower); flat with
+// noise textures: 5.  BVH: 5 (96 VGPRs; faster than 4 on the bunny, pawn and demo1 scenes).
+#ifndef RT_WAVES_FLAT
+#define RT_WAVES_FLAT 7
+#endif
+#ifndef RT_WAVES_FLAT_NOISE
+#define RT_WAVES_FLAT_NOISE 5
+#endif
+#ifndef RT_WAVES_BVH
+#define RT_WAVES_BVH 5
+#endif
+// knobs for the lightest instantiations (constant textures; BVH: no media): measured, 8 waves
+// for the Cornell kernel (62 VGPRs, 6 spilled) -0.3..0.7 %, 6 for the bunny's (80, 4 spilled) +3.4 %
+#ifndef RT_WAVES_FLAT_TEX0
+#define RT_WAVES_FLAT_TEX0 7
+#endif
+#ifndef RT_WAVES_BVH_LITE
+#define RT_WAVES_BVH_LITE 5
+#endif
+// binary64: every real is a register pair, so the same code needs about twice the VGPRs
+#ifndef RT_WAVES64_FLAT
+#define RT_WAVES64_FLAT 4
+#endif
+#ifndef RT_WAVES64_BVH
+#define RT_WAVES64_BVH 3
+#endif
+#if RT_F64
+#define RT_WAVES_OF(kVar, kTex, kMedia) ((kVar) == RT_VAR_FLAT ? RT_WAVES64_FLAT : RT_WAVES64_BVH)
+#else
+#define RT_WAVES_OF(kVar, kTex, kMedia)                                                                  \
+  ((kVar) == RT_VAR_FLAT ? ((kTex) == 2 ? RT_WAVES_FLAT_NOISE : (kTex) == 0 ? RT_WAVES_FLAT_TEX0 : RT_WAVES_FLAT) \
+                         : ((kTex) == 0 && !(kMedia) ? RT_WAVES_BVH_LITE : RT_WAVES_BVH))
+#endif
+template <int kVar, int kTex, bool kMedia, bool kMats>
+__global__ __launch_bounds__(kVar == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH)
+__attribute__((amdgpu_waves_per_eu(RT_WAVES_OF(kVar, kTex, kMedia))))
+void rt_render_kernel(KernelParams P) {
+  extern __shared__ int smem[];
+  // every wave starts with a static pool (its wave index x RT_POOL): at launch all resident waves
+  // would otherwise queue up on the counter at once (~80 us at ~88 returning atomics per us)
+  const int waves = (int)(gridDim.x * (blockDim.x / 64));
+  const int wave = (int)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
+  WaveGrab grab{P.counter, wave * RT_POOL, RT_POOL, waves * RT_POOL, P.n_items, wave & (RT_QUEUES - 1), 0};
+  AtomicCommit commit{P.accum, P.nanflag};
+  int overflow;
+  if constexpr (kVar == RT_VAR_FLAT) {
+    overflow =
+        lane_loop_lockstep<true, kTex, kMedia, kMats>(P, grab, commit, Trav{nullptr, 0, nullptr}, P.prims);
+  } else {
+    // LDS: [stack_depth + 1][RT_BLOCK_BVH] stack words (the last row a spare write target), then
+    // the top P.lds_nodes BVH nodes (64 B each)
+    v4f* lds_nodes = reinterpret_cast<v4f*>(smem + (P.stack_depth + 1) * RT_BLOCK_BVH);
+    const float4* src = reinterpret_cast<const float4*>(P.nodes);
+    for (int i = threadIdx.x; i < 4 * P.lds_nodes; i += RT_BLOCK_BVH) {
+      const float4 q = src[i];
+      lds_nodes[i] = v4f{q.x, q.y, q.z, q.w};
+    }
+    __syncthreads();
+    const Trav W{smem + threadIdx.x, RT_BLOCK_BVH, lds_nodes};
+    if constexpr (kVar == RT_VAR_BVH_LOCKSTEP)
+      overflow = lane_loop_lockstep<false, kTex, kMedia, kMats>(P, grab, commit, W, P.prims);
+    else
+      overflow = lane_loop_bvh<kTex, kMedia, kMats>(P, grab, commit, W, P.prims);
+  }
+  if (overflow) atomicOr(P.status, 1);
+}
+
+// mean over spp (Ray.hs:232) from the fixed-point sums; NaN where a sample was non-finite
+__global__ __launch_bounds__(256) void rt_resolve_kernel(const long long* __restrict__ accum,
+                                                         const unsigned int* __restrict__ nanflag,
+                                                         real* __restrict__ out, int n_pixels, int spp) {
+  int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n_pixels) return;
+  const bool bad = nanflag[i] != 0u;
+  const long long* a = accum + RT_ACC_WORDS(real) * (size_t)i;
+  for (int c = 0; c < 3; ++c) {
+#if RT_F64
+    // (hi + lo 2^-32) 2^-32 / spp: the integer words are exact in binary64 (< 2^53), one rounding
+    // for the sum, one for the mean
+    const double sum = ((double)a[c] + (double)(unsigned long long)a[3 + c] * (1.0 / RT_FIX_SCALE)) * (1.0 / RT_FIX_SCALE);
+    out[3 * (size_t)i + c] = bad ? __builtin_nan("") : sum / (double)spp;
+#else
+    out[3 * (size_t)i + c] = bad ? __builtin_nanf("") : (float)((double)a[c] * (1.0 / (RT_FIX_SCALE * (double)spp)));
+#endif
+  }
+}
+
+static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
+  return (variant & RT_VAR_BASE) == RT_VAR_FLAT ? 0
+                                                 : (size_t)(stack_depth + 1) * RT_BLOCK_BVH * sizeof(int) + (size_t)lds_nodes * 64;
+}
+
+// the kernel instantiation of a variant code (base variant | RT_VAR_TEX | RT_VAR_NOISE |
+// RT_VAR_MEDIA | RT_VAR_MATS): non-constant textures, noise textures, media and the materials
+// beyond lightSource / pitchBlack / lambertian are compiled only into the instantiations of
+// scenes that use them
+// (inlined everywhere it raises the register allocation of every scene's kernel: the Cornell
+// box is 4.8 % faster without the unused media code)
+typedef void (*render_fn)(KernelParams);
+template <int kVar, int kTex, bool kMedia>
+static render_fn render_kernel_mats(int variant) {
+  return (variant & RT_VAR_MATS) ? rt_render_kernel<kVar, kTex, kMedia, true> : rt_render_kernel<kVar, kTex, kMedia, false>;
+}
+template <int kVar, int kTex>
+static render_fn render_kernel_media(int variant) {
+  return (variant & RT_VAR_MEDIA) ? render_kernel_mats<kVar, kTex, true>(variant)
+                                  : render_kernel_mats<kVar, kTex, false>(variant);
+}
+template <int kVar>
+static render_fn render_kernel_flags(int variant) {
+  if (variant & RT_VAR_NOISE) return render_kernel_media<kVar, 2>(variant);
+  if (variant & RT_VAR_TEX) return render_kernel_media<kVar, 1>(variant);
+  return render_kernel_media<kVar, 0>(variant);
+}
+static render_fn render_kernel_of(int variant) {
+  switch (variant & RT_VAR_BASE) {
+    case RT_VAR_FLAT: return render_kernel_flags<RT_VAR_FLAT>(variant);
+    case RT_VAR_BVH_LOCKSTEP: return render_kernel_flags<RT_VAR_BVH_LOCKSTEP>(variant);
+    default: return render_kernel_flags<RT_VAR_BVH>(variant);
+  }
+}
+
+}  // namespace RT_NS
+
+int rt_render_resident_blocks(const KernelParamsT<RT_NS::real>*, int device, int stack_depth, int variant,
+                              int lds_nodes) {
+  using namespace RT_NS;
+  int per_cu = 0, cus = 0;
+  size_t lds = render_lds_bytes(stack_depth, variant, lds_nodes);
+  if (lds > 65536 && hipFuncSetAttribute((const void*)render_kernel_of(variant),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return -1;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_kernel_of(variant), rt_block_of(variant), lds);
+  if (e != hipSuccess) return -1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return -1;
+  if (per_cu < 1) per_cu = 1;
+  return per_cu * cus;
+}
+
+int rt_launch_render(const KernelParamsT<RT_NS::real>& p, int grid_blocks, int variant, void* stream) {
+  using namespace RT_NS;
+  if (p.n_items <= 0 || grid_blocks <= 0) return 0;
+  const int block = rt_block_of(variant);
+  long long need = ((long long)p.n_items + block - 1) / block;
+  int grid = need < grid_blocks ? (int)need : grid_blocks;
+  size_t lds = render_lds_bytes(p.stack_depth, variant, p.lds_nodes);
+  hipLaunchKernelGGL(render_kernel_of(variant), dim3(grid), dim3(block), lds, (hipStream_t)stream, p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int rt_launch_resolve(const KernelParamsT<RT_NS::real>& p, void* stream) {
+  using namespace RT_NS;
+  int n = p.tile_rows * p.cam.width;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(rt_resolve_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     (const long long*)p.accum, p.nanflag, p.out, n, p.cam.spp);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}

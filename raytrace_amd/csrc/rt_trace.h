@@ -20,15 +20,20 @@
 // in 64-bit fixed point (2^-32): integer addition commutes, so the mean (Ray.hs:232) is bit-for-
 // bit independent of chunking, scheduling and the multi-GPU row partition.
 //
-// FP32 arithmetic; Philox4x32-10 keyed by the seed with counter (pixel, sample, segment,
-// event) and 24-bit uniforms; direct samplers in place of the reference's rejection loops
-// (same distributions).  The FP64 oracle's Philox mode (oracle/rt_oracle.c) consumes the same
-// numbers, which is what the per-pixel parity tests check.
+// Precision: the header is instantiated twice, for `real` = double (RT_F64 = 1, namespace
+// rtk64: the reference's binary64 arithmetic, Core.hs:29-31; the default of the C ABI) and for
+// `real` = float (RT_F64 = 0, namespace rtk: the opt-in FP32 fast path).  The includer defines
+// RT_F64; a translation unit may include the header once per precision.  Philox4x32-10 keyed
+// by the seed with counter (pixel, sample, segment, event) and 24-bit uniforms; direct
+// samplers in place of the reference's rejection loops (same distributions).  The FP64
+// oracle's Philox mode (oracle/rt_oracle.c) consumes the same numbers, which is what the
+// per-pixel parity tests check.
 //
-// The header is compiled by hipcc for gfx950 (rt_kernel.hip).  tests/kernel_emu compiles the
+// The header is compiled by hipcc for gfx950 (rt_kernel.hip, rt_kernel64.hip).  tests/kernel_emu compiles the
 // same text for the host (RT_HOST_EMU) so the kernel's logic can be checked against the oracle
 // without a GPU; that build is test tooling and is never linked into the product library.
-#pragma once
+#ifndef RT_TRACE_COMMON_H
+#define RT_TRACE_COMMON_H
 #include <stdint.h>
 
 #include "../../include/rt.h"
@@ -49,11 +54,6 @@ inline int f2i(float f) {
 extern thread_local long long counters[4];
 }  // namespace rt_emu
 #define RT_F2I(f) rt_emu::f2i(f)
-#define RT_SINCOS_TURNS(x, s, c) (*(s) = sinf(6.283185307179586f * (x)), *(c) = cosf(6.283185307179586f * (x)))
-#define RT_LOG(x) logf(x)
-#define RT_RSQRT(x) (1.0f / sqrtf(x))
-#define RT_RCP(x) (1.0f / (x))
-#define RT_SQRT(x) sqrtf(x)
 #define RT_COUNT(i) (++rt_emu::counters[i])
 #define RT_ANY(x) (x)  // the emulator runs one lane per wave
 #define RT_BALLOT_COUNT(x) ((x) ? 1 : 0)
@@ -62,12 +62,6 @@ extern thread_local long long counters[4];
 #define RT_FN __device__ __forceinline__
 #define RT_FN_SPEC __device__ __forceinline__
 #define RT_F2I(f) __float_as_int(f)
-// sin / cos of 2 pi x for x in [0, 1): v_sin_f32 / v_cos_f32 take their argument in turns
-#define RT_SINCOS_TURNS(x, s, c) (*(s) = __builtin_amdgcn_sinf(x), *(c) = __builtin_amdgcn_cosf(x))
-#define RT_LOG(x) __logf(x)
-#define RT_RSQRT(x) __frsqrt_rn(x)
-#define RT_RCP(x) __builtin_amdgcn_rcpf(x)
-#define RT_SQRT(x) __builtin_amdgcn_sqrtf(x)  // v_sqrt_f32 (1 ulp), no IEEE fix-up sequence
 #define RT_COUNT(i) ((void)0)
 #define RT_ANY(x) __any(x)
 #define RT_BALLOT_COUNT(x) ((int)__popcll(__ballot(x)))
@@ -84,33 +78,133 @@ extern thread_local long long counters[4];
 #ifndef RT_HOOK_SAMPLE
 #define RT_HOOK_SAMPLE(pix, sample, L)
 #endif
+#endif  // RT_TRACE_COMMON_H
 
-namespace rtk {
+// ------------------------------------------------------------------ per-precision macros
+#ifndef RT_F64
+#define RT_F64 0
+#endif
+#undef RT_NS
+#undef RL
+#undef RMIN
+#undef RMAX
+#undef RABS
+#undef RFLOOR
+#undef RCOPYSIGN
+#undef RATAN2
+#undef RACOS
+#undef RSIN
+#undef RFMA
+#undef RT_NAN
+#undef RT_HUGE
+#undef RT_R2I
+#undef RT_SINCOS_TURNS
+#undef RT_LOG
+#undef RT_RSQRT
+#undef RT_RCP
+#undef RT_SQRT
+#if RT_F64
+// binary64: IEEE division and square root, libm / OCML transcendentals (the oracle's libm calls)
+#define RT_NS rtk64
+#define RL(x) x
+#define RMIN fmin
+#define RMAX fmax
+#define RABS fabs
+#define RFLOOR floor
+#define RCOPYSIGN copysign
+#define RATAN2 atan2
+#define RACOS acos
+#define RSIN sin
+#define RFMA fma
+#define RT_NAN __builtin_nan("")
+#define RT_HUGE __builtin_huge_val()
+// an int stored in a binary64 record: the low word of its bit pattern (rt_build.cpp ibits)
+#define RT_R2I(x) ((int)(uint32_t)__builtin_bit_cast(unsigned long long, (double)(x)))
+#define RT_SINCOS_TURNS(x, s, c) (*(s) = sin(6.283185307179586 * (x)), *(c) = cos(6.283185307179586 * (x)))
+#define RT_LOG(x) log(x)
+#define RT_RSQRT(x) (1.0 / sqrt(x))
+#define RT_RCP(x) (1.0 / (x))
+#define RT_SQRT(x) sqrt(x)
+#else
+#define RT_NS rtk
+#define RL(x) x##f
+#define RMIN fminf
+#define RMAX fmaxf
+#define RABS fabsf
+#define RFLOOR floorf
+#define RCOPYSIGN copysignf
+#define RATAN2 atan2f
+#define RACOS acosf
+#define RSIN sinf
+#define RFMA fmaf
+#define RT_NAN __builtin_nanf("")
+#define RT_HUGE __builtin_huge_valf()
+#define RT_R2I(x) RT_F2I(x)
+#ifdef RT_HOST_EMU
+#define RT_SINCOS_TURNS(x, s, c) (*(s) = sinf(6.283185307179586f * (x)), *(c) = cosf(6.283185307179586f * (x)))
+#define RT_LOG(x) logf(x)
+#define RT_RSQRT(x) (1.0f / sqrtf(x))
+#define RT_RCP(x) (1.0f / (x))
+#define RT_SQRT(x) sqrtf(x)
+#else
+// sin / cos of 2 pi x for x in [0, 1): v_sin_f32 / v_cos_f32 take their argument in turns
+#define RT_SINCOS_TURNS(x, s, c) (*(s) = __builtin_amdgcn_sinf(x), *(c) = __builtin_amdgcn_cosf(x))
+#define RT_LOG(x) __logf(x)
+#define RT_RSQRT(x) __frsqrt_rn(x)
+#define RT_RCP(x) __builtin_amdgcn_rcpf(x)
+#define RT_SQRT(x) __builtin_amdgcn_sqrtf(x)  // v_sqrt_f32 (1 ulp), no IEEE fix-up sequence
+#endif
+#endif
 
-constexpr float kPi = 3.14159265358979323846f;
-constexpr float kTmin = 0.0001f;  // Ray.hs:178
-constexpr float kInf = __builtin_huge_valf();
+namespace RT_NS {
 
-struct alignas(16) v4 {
+#if RT_F64
+using real = double;
+#else
+using real = float;
+#endif
+using KernelParams = ::KernelParamsT<real>;
+using DevMaterial = ::DevMaterialT<real>;
+using DevTexture = ::DevTextureT<real>;
+using DevMedium = ::DevMediumT<real>;
+using DevBox = ::DevBoxT<real>;
+using DevTarget = ::DevTargetT<real>;
+using DevCamera = ::DevCameraT<real>;
+
+
+
+constexpr real kPi = RL(3.14159265358979323846);
+constexpr real kTmin = RL(0.0001);  // Ray.hs:178
+constexpr real kInf = RT_HUGE;
+
+struct alignas(4 * sizeof(real)) v4 {
+  real x, y, z, w;
+};
+struct alignas(16) v4f {  // BVH node data (float in both precisions)
   float x, y, z, w;
 };
 struct alignas(16) i4 {
   int x, y, z, w;
 };
 struct f3 {
-  float x, y, z;
+  real x, y, z;
 };
-RT_FN f3 mk3(float x, float y, float z) { return f3{x, y, z}; }
-RT_FN f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
+RT_FN f3 mk3(real x, real y, real z) { return f3{x, y, z}; }
+RT_FN f3 ld3(const real* p) { return f3{p[0], p[1], p[2]}; }
 RT_FN f3 operator+(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
 RT_FN f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 RT_FN f3 operator-(f3 a) { return f3{-a.x, -a.y, -a.z}; }
-RT_FN f3 operator*(float s, f3 a) { return f3{s * a.x, s * a.y, s * a.z}; }
+RT_FN f3 operator*(real s, f3 a) { return f3{s * a.x, s * a.y, s * a.z}; }
 RT_FN f3 operator*(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
-RT_FN float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+RT_FN real dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 RT_FN f3 normalize(f3 v) {
-  float l = dot(v, v);
-  if (l <= 1e-12f) return v;  // linear's normalize leaves (near-)zero vectors alone
+  real l = dot(v, v);
+#if RT_F64
+  // linear's normalize: v unchanged when its quadrance is nearZero or nearZero (1 - quadrance)
+  if (RABS(l) <= RL(1e-12) || RABS(RL(1.0) - l) <= RL(1e-12)) return v;
+#else
+  if (l <= RL(1e-12)) return v;  // linear's normalize leaves (near-)zero vectors alone
+#endif
   return RT_RSQRT(l) * v;
 }
 // Re-normalise a direction that is unit in exact arithmetic (reflect / refract of unit vectors,
@@ -120,17 +214,22 @@ RT_FN f3 normalize(f3 v) {
 // surface, the normal (p - c) / r is no longer unit, reflect lengthens d) until the path
 // diverges.  Re-normalising keeps the FP32 path on the exact-arithmetic result.
 RT_FN f3 unit(f3 v) { return RT_RSQRT(dot(v, v)) * v; }
-RT_FN f3 reflect(f3 n, f3 v) { return v - (2.0f * dot(n, v)) * n; }  // Core.hs:49-51
+RT_FN f3 reflect(f3 n, f3 v) { return v - (RL(2.0) * dot(n, v)) * n; }  // Core.hs:49-51
 RT_FN f3 xyz(v4 v) { return f3{v.x, v.y, v.z}; }
-RT_FN v4 ld4(const float* p) { return *reinterpret_cast<const v4*>(p); }
-typedef const RT_CAS float* cfp;  // pointer to read-only scene data
-RT_FN cfp cf(const float* p) { return (cfp)p; }
+RT_FN v4 ld4(const real* p) { return *reinterpret_cast<const v4*>(p); }
+typedef const RT_CAS real* cfp;  // pointer to read-only scene data
+RT_FN cfp cf(const real* p) { return (cfp)p; }
 RT_FN f3 ldc3(cfp p) { return f3{p[0], p[1], p[2]}; }
 RT_FN v4 ldc4(cfp p) {
   const RT_CAS v4* q = (const RT_CAS v4*)p;
   return v4{q->x, q->y, q->z, q->w};
 }
 RT_FN int ldci(const int* p, int i) { return ((const RT_CAS int*)p)[i]; }
+typedef const RT_CAS float* cfpf;  // BVH nodes
+RT_FN v4f ldc4f(cfpf p) {
+  const RT_CAS v4f* q = (const RT_CAS v4f*)p;
+  return v4f{q->x, q->y, q->z, q->w};
+}
 
 // ------------------------------------------------------------------ Philox4x32-10
 struct u4 {
@@ -164,16 +263,16 @@ RT_FN u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
   return u4{c0, c1, c2, c3};
 }
 // [0, 1) with 24 random bits: exact in both FP32 and the oracle's FP64
-RT_FN float u01(uint32_t w) { return (float)(w >> 8) * (1.0f / 16777216.0f); }
+RT_FN real u01(uint32_t w) { return (real)(w >> 8) * (RL(1.0) / RL(16777216.0)); }
 
 // uniform direction on the unit sphere (the distribution of randomUnitVector, Core.hs:54-60)
 RT_FN f3 unit_vector(uint32_t a, uint32_t b) {
-  float z = 1.0f - 2.0f * u01(a);
-  float r = RT_SQRT(fmaxf(0.0f, 1.0f - z * z));
-  float s, c;
+  real z = RL(1.0) - RL(2.0) * u01(a);
+  real r = RT_SQRT(RMAX(RL(0.0), RL(1.0) - z * z));
+  real s, c;
 #ifdef RT_EXP_NO_SINCOS  // ablation: wrong directions, measures the cost of sincos
-  c = 1.0f - 2.0f * u01(b);
-  s = RT_SQRT(fmaxf(0.0f, 1.0f - c * c));
+  c = RL(1.0) - RL(2.0) * u01(b);
+  s = RT_SQRT(RMAX(RL(0.0), RL(1.0) - c * c));
 #else
   RT_SINCOS_TURNS(u01(b), &s, &c);
 #endif
@@ -182,37 +281,50 @@ RT_FN f3 unit_vector(uint32_t a, uint32_t b) {
 
 struct RayCtx {
   f3 o, d, idir, oidir;
-  float time;
+  real time;
   int self_gid;
 };
 
-RT_FN f3 motion_shift(const KernelParams& P, int m, float time) {
+RT_FN f3 motion_shift(const KernelParams& P, int m, real time) {
   f3 v0 = ldc3(cf(P.motions) + 8 * m), v1 = ldc3(cf(P.motions) + 8 * m + 4);
-  return (1.0f - time) * v0 + time * v1;
+  return (RL(1.0) - time) * v0 + time * v1;
 }
 
-RT_FN float safe_rcp(float d) { return RT_RCP(fabsf(d) > 1e-20f ? d : copysignf(1e-20f, d)); }
+RT_FN real safe_rcp(real d) { return RT_RCP(RABS(d) > RL(1e-20) ? d : RCOPYSIGN(RL(1e-20), d)); }
 
-// Closest hit so far.  key = (bits of t) << 32 | depth-first order: for t > 0 the integer
-// order of the key is the reference's closest-hit rule — smaller t, ties to the earlier leaf
-// (Geometry.hs:340-361) — so one 64-bit compare replaces the t / tie / validity mask logic.
-// Invalid candidates carry t = NaN (bits above +inf); the initial key is (+inf, 0).
+// Closest hit so far, keyed by (t, depth-first order): smaller t wins, ties go to the earlier
+// leaf (Geometry.hs:340-361).  Float kernels pack the key into 64 bits, (bits of t) << 32 |
+// order: for t > 0 its integer order is that rule, so one 64-bit compare replaces the t / tie /
+// validity mask logic; invalid candidates carry t = NaN (bits above +inf), the initial key is
+// (+inf, 0).  Binary64 kernels compare (t, order) as a pair.
+#if RT_F64
 struct Closest {
-  float t;
+  real t;
+  int ord;
+  int prim;
+};
+#else
+struct Closest {
+  real t;
   unsigned long long key;
   int prim;
 };
+#endif
 // Per-lane traversal resources: the lane's stack (stack[k * stride]) and the workgroup's LDS copy
 // of the first P.lds_nodes BVH nodes (breadth-first numbering puts the top levels there).
 struct Trav {
   int* stack;
   int stride;
-  const v4* lds_nodes;
+  const v4f* lds_nodes;
 };
+#if RT_F64
+RT_FN Closest no_hit() { return Closest{kInf, 0, -1}; }
+#else
 RT_FN Closest no_hit() { return Closest{kInf, 0x7f80000000000000ull, -1}; }
-RT_FN unsigned long long hit_key(float t, int ord) {
+RT_FN unsigned long long hit_key(real t, int ord) {
   return ((unsigned long long)(unsigned)RT_F2I(t) << 32) | (unsigned)ord;
 }
+#endif
 
 // A primitive record (rt_internal.h layout, 64 B): a = (center | normal, kind+flags),
 // b = (radius, r^2, uvframe, gid | q, gid), c = (-, -, -, order | wa, order), e = (wb, motion).
@@ -220,60 +332,70 @@ struct PrimRec {
   v4 a, b, c, e;
 };
 RT_FN PrimRec ld_rec(cfp pr) { return PrimRec{ldc4(pr), ldc4(pr + 4), ldc4(pr + 8), ldc4(pr + 12)}; }
-struct alignas(64) PrimRec64 {
-  float f[16];
+struct alignas(16 * sizeof(real)) PrimRec64 {  // one record: 64 B (float) / 128 B (binary64)
+  real f[16];
 };
 RT_FN PrimRec ld_rec64(const RT_CAS PrimRec64* p) {
-  const RT_CAS float* r = p->f;
+  const RT_CAS real* r = p->f;
   return PrimRec{v4{r[0], r[1], r[2], r[3]}, v4{r[4], r[5], r[6], r[7]}, v4{r[8], r[9], r[10], r[11]},
                  v4{r[12], r[13], r[14], r[15]}};
 }
 
 // Primitive intersection (Geometry.hs:58-144), branch-free: each test yields a parameter t and
 // one validity margin q (valid iff q >= 0) that also carries the interval test t > tmin as
-// t - up(tmin) >= 0 (up = next float: exact for the open interval), so the closest-hit update is
+// t - up(tmin) >= 0 (up = next real: exact for the open interval), so the closest-hit update is
 // a single compare and select with no per-test lane-mask bookkeeping on the scalar unit.
-RT_FN float float_up(float x) { return __builtin_bit_cast(float, RT_F2I(x) + 1); }  // x > 0
+#if RT_F64
+RT_FN real float_up(real x) { return __builtin_bit_cast(real, __builtin_bit_cast(long long, x) + 1); }  // x > 0
+#else
+RT_FN real float_up(real x) { return __builtin_bit_cast(real, RT_F2I(x) + 1); }  // x > 0
+#endif
 // sphere (Geometry.hs:58-94); geometric discriminant for FP32 robustness.  A ray leaving this
 // sphere (self) can only reach the far root 2h (the near one is t = 0).
-RT_FN void isect_sphere(const PrimRec& r, f3 o, const RayCtx& R, float tmin, float tmin_up, bool self, float& t,
-                        float& q) {
+RT_FN void isect_sphere(const PrimRec& r, f3 o, const RayCtx& R, real tmin, real tmin_up, bool self, real& t,
+                        real& q) {
   f3 oc = xyz(r.a) - o;
-  float h = dot(R.d, oc);
+  real h = dot(R.d, oc);
   f3 l = oc - h * R.d;
-  float disc = r.b.y - dot(l, l);
-  float sq = RT_SQRT(fmaxf(disc, 0.0f));
-  float r1 = h - sq, r2 = h + sq;
-  float tn = r1 > tmin ? r1 : r2;
-  t = self ? 2.0f * h : tn;
-  q = fminf(self ? 1.0f : disc, t - tmin_up);
+  real disc = r.b.y - dot(l, l);
+  real sq = RT_SQRT(RMAX(disc, RL(0.0)));
+  real r1 = h - sq, r2 = h + sq;
+  real tn = r1 > tmin ? r1 : r2;
+  t = self ? RL(2.0) * h : tn;
+  q = RMIN(self ? RL(1.0) : disc, t - tmin_up);
 }
 // planeShape (Geometry.hs:117-144): parallelogram a, b in [0,1]; triangle a, b >= 0, a + b <= 1.
 // kQuad: 1 parallelogram, 0 triangle, -1 either (per-lane `quad`, a select instead of a branch)
 template <int kQuad>
-RT_FN void isect_plane(const PrimRec& r, f3 o, const RayCtx& R, float tmin_up, bool self, float& t, float& q,
+RT_FN void isect_plane(const PrimRec& r, f3 o, const RayCtx& R, real tmin_up, bool self, real& t, real& q,
                        bool quad = false) {
   f3 n = xyz(r.a);
-  float denom = dot(n, R.d);
+  real denom = dot(n, R.d);
   f3 qo = xyz(r.b) - o;
   t = dot(n, qo) * RT_RCP(denom);
   f3 prel = t * R.d - qo;
-  float aa = dot(prel, xyz(r.c)), bb = dot(prel, xyz(r.e));
-  float m1, m2 = fminf(fabsf(denom) - 1e-8f, t - tmin_up);
+  real aa = dot(prel, xyz(r.c)), bb = dot(prel, xyz(r.e));
+  real m1, m2 = RMIN(RABS(denom) - RL(1e-8), t - tmin_up);
   if constexpr (kQuad < 0) {  // quad: min(1 - a, 1 - b); triangle: 1 - a - b
-    m1 = fminf(fminf(aa, bb), quad ? fminf(1.0f - aa, 1.0f - bb) : 1.0f - aa - bb);
+    m1 = RMIN(RMIN(aa, bb), quad ? RMIN(RL(1.0) - aa, RL(1.0) - bb) : RL(1.0) - aa - bb);
   } else if constexpr (kQuad == 1) {
-    m1 = fminf(fminf(aa, bb), 1.0f - aa);
-    m2 = fminf(m2, 1.0f - bb);
+    m1 = RMIN(RMIN(aa, bb), RL(1.0) - aa);
+    m2 = RMIN(m2, RL(1.0) - bb);
   } else {
-    m1 = fminf(fminf(aa, bb), 1.0f - aa - bb);
+    m1 = RMIN(RMIN(aa, bb), RL(1.0) - aa - bb);
   }
-  q = self ? -1.0f : fminf(m1, m2);
+  q = self ? -RL(1.0) : RMIN(m1, m2);
 }
 // kKeyOnly (flat sets): only the key is tracked; t and the primitive follow from it afterwards
 template <bool kKeyOnly>
-RT_FN void consider(Closest& C, float t, float q, int ord, int pi) {
-  const float tc = q >= 0.0f ? t : __builtin_nanf("");
+RT_FN void consider(Closest& C, real t, real q, int ord, int pi) {
+#if RT_F64
+  const bool take = q >= RL(0.0) && (t < C.t || (t == C.t && ord < C.ord));
+  C.t = take ? t : C.t;
+  C.ord = take ? ord : C.ord;
+  if constexpr (!kKeyOnly) C.prim = take ? pi : C.prim;
+#else
+  const real tc = q >= RL(0.0) ? t : RT_NAN;
   const unsigned long long key = hit_key(tc, ord);
   const bool take = key < C.key;
   C.key = take ? key : C.key;
@@ -281,19 +403,20 @@ RT_FN void consider(Closest& C, float t, float q, int ord, int pi) {
     C.t = take ? tc : C.t;
     C.prim = take ? pi : C.prim;
   }
+#endif
 }
 
 // Any primitive record against the open interval (tmin, C.t).  When the record is wave-uniform
 // (flat sets) it sits in SGPRs and the kind / motion tests are scalar branches.
 template <bool kKeyOnly = false>
-RT_FN void test_rec(const KernelParams& P, const PrimRec& r, int pi, const RayCtx& R, float tmin, float tmin_up,
+RT_FN void test_rec(const KernelParams& P, const PrimRec& r, int pi, const RayCtx& R, real tmin, real tmin_up,
                     Closest& C) {
   RT_COUNT(1);
-  const int kf = RT_F2I(r.a.w);
+  const int kf = RT_R2I(r.a.w);
   f3 o = R.o;
-  if (kf & RT_FLAG_MOTION) o = o - motion_shift(P, RT_F2I(r.e.w), R.time);
-  const bool self = RT_F2I(r.b.w) == R.self_gid;
-  float t, q;
+  if (kf & RT_FLAG_MOTION) o = o - motion_shift(P, RT_R2I(r.e.w), R.time);
+  const bool self = RT_R2I(r.b.w) == R.self_gid;
+  real t, q;
   if ((kf & RT_KIND_MASK) == 0)
     isect_sphere(r, o, R, tmin, tmin_up, self, t, q);
   else if constexpr (!kKeyOnly)  // BVH leaves: parallelograms and triangles share one path
@@ -302,20 +425,20 @@ RT_FN void test_rec(const KernelParams& P, const PrimRec& r, int pi, const RayCt
     isect_plane<1>(r, o, R, tmin_up, self, t, q);
   else
     isect_plane<0>(r, o, R, tmin_up, self, t, q);
-  consider<kKeyOnly>(C, t, q, RT_F2I(r.c.w), pi);
+  consider<kKeyOnly>(C, t, q, RT_R2I(r.c.w), pi);
 }
 
 // A static primitive of a known kind (flat sets are grouped by class: rt_build.cpp).
 template <int kKind, bool kKeyOnly = true>
-RT_FN void test_static(const PrimRec& r, const RayCtx& R, float tmin, float tmin_up, Closest& C, int pi = 0) {
+RT_FN void test_static(const PrimRec& r, const RayCtx& R, real tmin, real tmin_up, Closest& C, int pi = 0) {
   RT_COUNT(1);
-  const bool self = RT_F2I(r.b.w) == R.self_gid;
-  float t, q;
+  const bool self = RT_R2I(r.b.w) == R.self_gid;
+  real t, q;
   if constexpr (kKind == RT_PRIM_CLASS_SPHERE)
     isect_sphere(r, R.o, R, tmin, tmin_up, self, t, q);
   else
     isect_plane<kKind == RT_PRIM_CLASS_QUAD ? 1 : 0>(r, R.o, R, tmin_up, self, t, q);
-  consider<kKeyOnly>(C, t, q, RT_F2I(r.c.w), pi);
+  consider<kKeyOnly>(C, t, q, RT_R2I(r.c.w), pi);
 }
 
 // A box group (rt_internal.h DevBox): slabs in the box frame give the entry and exit points of
@@ -329,51 +452,51 @@ RT_FN int box_field(int base, int code, int f, bool& present) {
 }
 // a face's key order, its primitive and whether the hit on it is valid (margin q >= 0, the face
 // exists, and it is not the face the ray leaves)
-RT_FN bool box_face(const RT_CAS DevBox* B, int f, float q, const RayCtx& R, int& ord, int& prim, bool with_prim) {
+RT_FN bool box_face(const RT_CAS DevBox* B, int f, real q, const RayCtx& R, int& ord, int& prim, bool with_prim) {
   bool present;
   ord = box_field(B->ord_base, B->ord_code, f, present);
   const int gid = box_field(B->gid_base, B->gid_code, f, present);
   if (with_prim) prim = box_field(B->prim_base, B->prim_code, f, present);
-  return present && gid != R.self_gid && q >= 0.0f;
+  return present && gid != R.self_gid && q >= RL(0.0);
 }
 template <bool kKeyOnly>
-RT_FN void test_box(const RT_CAS DevBox* B, const RayCtx& R, float tmin_up, Closest& C) {
+RT_FN void test_box(const RT_CAS DevBox* B, const RayCtx& R, real tmin_up, Closest& C) {
   RT_COUNT(1);
   const f3 oc = R.o - f3{B->c[0], B->c[1], B->c[2]};
   const f3 ax[3] = {f3{B->a0[0], B->a0[1], B->a0[2]}, f3{B->a1[0], B->a1[1], B->a1[2]},
                     f3{B->a2[0], B->a2[1], B->a2[2]}};
-  float lo[3], hi[3];
+  real lo[3], hi[3];
   int flip[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const float inv = RT_RCP(dot(ax[k], R.d));
-    const float s = dot(ax[k], oc);
-    const float t0 = -s * inv, t1 = fmaf(-s, inv, inv);  // the s = 0 and s = 1 planes
+    const real inv = RT_RCP(dot(ax[k], R.d));
+    const real s = dot(ax[k], oc);
+    const real t0 = -s * inv, t1 = RFMA(-s, inv, inv);  // the s = 0 and s = 1 planes
     flip[k] = t1 < t0 ? 1 : 0;                            // entering through the s = 1 end
-    lo[k] = fminf(t0, t1);
-    hi[k] = fmaxf(t0, t1);
+    lo[k] = RMIN(t0, t1);
+    hi[k] = RMAX(t0, t1);
   }
-  const float tn = fmaxf(fmaxf(lo[0], lo[1]), lo[2]), tf = fminf(fminf(hi[0], hi[1]), hi[2]);
+  const real tn = RMAX(RMAX(lo[0], lo[1]), lo[2]), tf = RMIN(RMIN(hi[0], hi[1]), hi[2]);
   const int an = lo[0] == tn ? 0 : lo[1] == tn ? 1 : 2;
   const int af = hi[0] == tf ? 0 : hi[1] == tf ? 1 : 2;
   const int fn = 2 * an + (an == 0 ? flip[0] : an == 1 ? flip[1] : flip[2]);
   const int ff = 2 * af + 1 - (af == 0 ? flip[0] : af == 1 ? flip[1] : flip[2]);
-  const float gap = tf - tn;  // >= 0: the line meets the box
+  const real gap = tf - tn;  // >= 0: the line meets the box
   // the entry point is nearer than the exit point: the exit matters only when the entry is not
   // a valid hit (one key compare per box)
   int ord_n, ord_f, prim_n = 0, prim_f = 0;
-  const bool vn = box_face(B, fn, fminf(gap, tn - tmin_up), R, ord_n, prim_n, !kKeyOnly);
-  const bool vf = box_face(B, ff, fminf(gap, tf - tmin_up), R, ord_f, prim_f, !kKeyOnly);
-  consider<kKeyOnly>(C, vn ? tn : tf, (vn || vf) ? 0.0f : -1.0f, vn ? ord_n : ord_f, vn ? prim_n : prim_f);
+  const bool vn = box_face(B, fn, RMIN(gap, tn - tmin_up), R, ord_n, prim_n, !kKeyOnly);
+  const bool vf = box_face(B, ff, RMIN(gap, tf - tmin_up), R, ord_f, prim_f, !kKeyOnly);
+  consider<kKeyOnly>(C, vn ? tn : tf, (vn || vf) ? RL(0.0) : -RL(1.0), vn ? ord_n : ord_f, vn ? prim_n : prim_f);
 }
 
 // BVH scenes: the surface set's large-primitive prefix (rt_build.cpp; P.flat_sets[0]), tested
 // before the traversal so that its closest hit bounds it.  The range is a kernel argument, so
 // the records are wave-uniform (scalar loads) even when only some lanes start a query here.
-RT_FN void prefix_hits(const KernelParams& P, cfp prims, const RayCtx& R, float tmin, Closest& C) {
+RT_FN void prefix_hits(const KernelParams& P, cfp prims, const RayCtx& R, real tmin, Closest& C) {
   const DevFlatSet& S = P.flat_sets[0];
   if (!P.surface_prefix || (S.end == S.first && S.box_end == S.box_first)) return;
-  const float tmin_up = float_up(tmin);
+  const real tmin_up = float_up(tmin);
   for (int b = S.box_first; b < S.box_end; ++b) test_box<false>((const RT_CAS DevBox*)P.boxes + b, R, tmin_up, C);
   int k = S.first;
   const RT_CAS PrimRec64* rp = (const RT_CAS PrimRec64*)prims + k;
@@ -388,69 +511,69 @@ RT_FN void prefix_hits(const KernelParams& P, cfp prims, const RayCtx& R, float 
 // leaves at most): every lane walks the same records in the same order, so the loop is coherent
 // and the records are read with scalar loads (uniform addresses).
 template <bool kFlat>
-RT_FN void closest(const KernelParams& P, cfp prims, int root, int set, const RayCtx& R, float tmin, Closest& C,
+RT_FN void closest(const KernelParams& P, cfp prims, int root, int set, const RayCtx& R, real tmin, Closest& C,
                    const Trav& W, int* overflow);
 
 struct HitInfo {
   f3 p, n;
   bool front;
-  float u, v;
+  real u, v;
   int gid;
 };
 
 // front side of a boundary hit (constantMedium's case split, Geometry.hs:308)
-RT_FN bool prim_front(const KernelParams& P, cfp prims, int pi, const RayCtx& R, float t) {
+RT_FN bool prim_front(const KernelParams& P, cfp prims, int pi, const RayCtx& R, real t) {
   cfp pr = prims + 16 * (size_t)pi;
   v4 a = ldc4(pr);
-  int kf = RT_F2I(a.w);
+  int kf = RT_R2I(a.w);
   if ((kf & RT_KIND_MASK) == 0) {
     f3 c = xyz(a);
-    if (kf & RT_FLAG_MOTION) c = c + motion_shift(P, RT_F2I(pr[15]), R.time);
+    if (kf & RT_FLAG_MOTION) c = c + motion_shift(P, RT_R2I(pr[15]), R.time);
     f3 p = R.o + t * R.d;
-    return dot(R.d, p - c) * (pr[4] < 0.0f ? -1.0f : 1.0f) <= 0.0f;
+    return dot(R.d, p - c) * (pr[4] < RL(0.0) ? -RL(1.0) : RL(1.0)) <= RL(0.0);
   }
-  return dot(xyz(a), R.d) < 0.0f;
+  return dot(xyz(a), R.d) < RL(0.0);
 }
 
 // need_uv: the material reads a (u, v) texture; otherwise the texture coordinates (sphereUV's
 // atan2 / acos, the triangle's uv lerp and its prim_uv loads) are skipped.
-RT_FN HitInfo surface_info(const KernelParams& P, cfp prims, int pi, const RayCtx& R, float t, bool need_uv) {
+RT_FN HitInfo surface_info(const KernelParams& P, cfp prims, int pi, const RayCtx& R, real t, bool need_uv) {
   HitInfo h;
   cfp pr = prims + 16 * (size_t)pi;
   v4 a = ldc4(pr), b = ldc4(pr + 4);
-  int kf = RT_F2I(a.w);
+  int kf = RT_R2I(a.w);
   h.p = R.o + t * R.d;
-  h.gid = RT_F2I(b.w);
+  h.gid = RT_R2I(b.w);
   if ((kf & RT_KIND_MASK) == 0) {
     f3 c = xyz(a);
-    if (kf & RT_FLAG_MOTION) c = c + motion_shift(P, RT_F2I(pr[15]), R.time);
+    if (kf & RT_FLAG_MOTION) c = c + motion_shift(P, RT_R2I(pr[15]), R.time);
     f3 outward = RT_RCP(b.x) * (h.p - c);
-    h.front = dot(R.d, outward) <= 0.0f;
+    h.front = dot(R.d, outward) <= RL(0.0);
     h.n = h.front ? outward : -outward;
-    h.u = h.v = 0.0f;
+    h.u = h.v = RL(0.0);
     if (!need_uv) return h;
-    int uvf = RT_F2I(b.z);
+    int uvf = RT_R2I(b.z);
     f3 on = outward;
     if (uvf >= 0) {
       cfp fr = cf(P.uvframes) + 12 * uvf;
       on = mk3(dot(ldc3(fr), outward), dot(ldc3(fr + 4), outward), dot(ldc3(fr + 8), outward));
     }
     // sphereUV (Geometry.hs:100-104)
-    h.u = atan2f(on.x, on.z) * (0.5f / kPi) + 0.5f;
-    h.v = acosf(fminf(1.0f, fmaxf(-1.0f, -on.y))) * (1.0f / kPi);
+    h.u = RATAN2(on.x, on.z) * (RL(0.5) / kPi) + RL(0.5);
+    h.v = RACOS(RMIN(RL(1.0), RMAX(-RL(1.0), -on.y))) * (RL(1.0) / kPi);
   } else {
     f3 n = xyz(a);
-    float denom = dot(n, R.d);
-    h.front = denom < 0.0f;
+    real denom = dot(n, R.d);
+    h.front = denom < RL(0.0);
     h.n = h.front ? n : -n;
-    h.u = h.v = 0.0f;
+    h.u = h.v = RL(0.0);
     if (!need_uv) return h;
     f3 o = R.o;
-    if (kf & RT_FLAG_MOTION) o = o - motion_shift(P, RT_F2I(pr[15]), R.time);
+    if (kf & RT_FLAG_MOTION) o = o - motion_shift(P, RT_R2I(pr[15]), R.time);
     f3 prel = (o + t * R.d) - xyz(b);
-    float aa = dot(prel, ldc3(pr + 8)), bb = dot(prel, ldc3(pr + 12));
+    real aa = dot(prel, ldc3(pr + 8)), bb = dot(prel, ldc3(pr + 12));
     cfp uv = cf(P.prim_uv) + 6 * (size_t)pi;
-    float w0 = 1.0f - aa - bb;
+    real w0 = RL(1.0) - aa - bb;
     h.u = w0 * uv[0] + aa * uv[2] + bb * uv[4];
     h.v = w0 * uv[1] + aa * uv[3] + bb * uv[5];
   }
@@ -460,30 +583,30 @@ RT_FN HitInfo surface_info(const KernelParams& P, cfp prims, int pi, const RayCt
 // Perlin noise (Noise.hs:21-45): gradients at the 8 lattice corners, smoothstep weights.
 // Kept compact (corner loop not unrolled) so the rarely used noise textures do not raise the
 // register allocation of the whole lane loop.
-RT_FN float smooth3(float x) { return x * x * (3.0f - 2.0f * x); }
-RT_FN float perlin_noise(const RT_CAS int* perm, cfp grad, f3 p) {
-  const float x0 = floorf(p.x), y0 = floorf(p.y), z0 = floorf(p.z);
+RT_FN real smooth3(real x) { return x * x * (RL(3.0) - RL(2.0) * x); }
+RT_FN real perlin_noise(const RT_CAS int* perm, cfp grad, f3 p) {
+  const real x0 = RFLOOR(p.x), y0 = RFLOOR(p.y), z0 = RFLOOR(p.z);
   const int ix = (int)x0, iy = (int)y0, iz = (int)z0;
-  const float fx = p.x - x0, fy = p.y - y0, fz = p.z - z0;
-  float sum = 0.0f;
+  const real fx = p.x - x0, fy = p.y - y0, fz = p.z - z0;
+  real sum = RL(0.0);
 #pragma unroll 1
   for (int c = 0; c < 8; ++c) {
     const int i = c >> 2, j = (c >> 1) & 1, k = c & 1;
     const int g = perm[(ix + i) & 255] ^ perm[256 + ((iy + j) & 255)] ^ perm[512 + ((iz + k) & 255)];
-    const float rx = fx - (float)i, ry = fy - (float)j, rz = fz - (float)k;
-    const float w = smooth3(i ? fx : 1.0f - fx) * smooth3(j ? fy : 1.0f - fy) * smooth3(k ? fz : 1.0f - fz);
+    const real rx = fx - (real)i, ry = fy - (real)j, rz = fz - (real)k;
+    const real w = smooth3(i ? fx : RL(1.0) - fx) * smooth3(j ? fy : RL(1.0) - fy) * smooth3(k ? fz : RL(1.0) - fz);
     sum += w * dot(ldc3(grad + 4 * g), mk3(rx, ry, rz));
   }
   return sum;
 }
 // fractalNoise (Noise.hs:48-53): layers of doubling frequency and halving weight
-RT_FN float fractal_noise(const RT_CAS int* perm, cfp grad, int depth, f3 p) {
-  float sum = 0.0f, w = 1.0f;
+RT_FN real fractal_noise(const RT_CAS int* perm, cfp grad, int depth, f3 p) {
+  real sum = RL(0.0), w = RL(1.0);
 #pragma unroll 1
   for (int l = 0; l < depth; ++l) {
     sum += w * perlin_noise(perm, grad, p);
-    w *= 0.5f;
-    p = 2.0f * p;
+    w *= RL(0.5);
+    p = RL(2.0) * p;
   }
   return sum;
 }
@@ -494,32 +617,32 @@ RT_FN f3 eval_noise_texture(const RT_CAS int* perm, cfp grad, const RT_CAS DevTe
   f3 c0 = f3{T->c0[0], T->c0[1], T->c0[2]};
   if (T->kind == RT_TEX_NOISE) {  // noiseTexture (Texture.hs:56-67)
     const f3 q = T->prm[0] * p + mk3(T->prm[1], T->prm[2], T->prm[3]);
-    const float n = fractal_noise(perm, grad, T->nu, q) * (0.5f / 0.8f) + 0.5f;
+    const real n = fractal_noise(perm, grad, T->nu, q) * (RL(0.5) / RL(0.8)) + RL(0.5);
     return c0 + n * (f3{T->c1[0], T->c1[1], T->c1[2]} - c0);
   }
   // marbleTexture (Texture.hs:70-78)
-  const float freq = T->prm[3];
-  const float arg = freq * dot(mk3(T->prm[0], T->prm[1], T->prm[2]), p);
-  const float turb =
-      fabsf(fractal_noise(perm, grad, 7, (0.25f * freq) * p + mk3(T->prm[4], T->prm[5], T->prm[6])));
-  const float m = 0.5f + 0.5f * sinf(arg + 10.0f * turb);
+  const real freq = T->prm[3];
+  const real arg = freq * dot(mk3(T->prm[0], T->prm[1], T->prm[2]), p);
+  const real turb =
+      RABS(fractal_noise(perm, grad, 7, (RL(0.25) * freq) * p + mk3(T->prm[4], T->prm[5], T->prm[6])));
+  const real m = RL(0.5) + RL(0.5) * RSIN(arg + RL(10.0) * turb);
   return mk3(m, m, m);
 }
 
 // Textures (Texture.hs:18-78); (u, v) for uv textures, the hit point p for solid ones
 template <bool kNoise>
-RT_FN f3 eval_texture(const KernelParams& P, int tex, float u, float v, f3 p) {
+RT_FN f3 eval_texture(const KernelParams& P, int tex, real u, real v, f3 p) {
   const RT_CAS DevTexture* T = (const RT_CAS DevTexture*)P.texs + tex;
   const int kind = T->kind;
   f3 c0 = f3{T->c0[0], T->c0[1], T->c0[2]};
   if (kind == RT_TEX_CONSTANT) return c0;
   if (kind == RT_TEX_CHECKER) {  // checkerTexture (Texture.hs:45-53)
-    int i = (int)floorf(u * (float)T->nu), j = (int)floorf(v * (float)T->nv);
+    int i = (int)RFLOOR(u * (real)T->nu), j = (int)RFLOOR(v * (real)T->nv);
     return ((i + j) & 1) == 0 ? c0 : f3{T->c1[0], T->c1[1], T->c1[2]};
   }
   if (kind == RT_TEX_IMAGE) {  // imageTexture (Texture.hs:31-41): wrap, v = 0 at the bottom row
     const int w = T->nu, h = T->nv;
-    int i = (int)floorf(u * (float)w) % w, j = (int)floorf((1.0f - v) * (float)h) % h;
+    int i = (int)RFLOOR(u * (real)w) % w, j = (int)RFLOOR((RL(1.0) - v) * (real)h) % h;
     i += i < 0 ? w : 0;
     j += j < 0 ? h : 0;
     return ldc3(cf(P.texels) + 4 * ((size_t)T->off + (size_t)j * w + i));
@@ -529,21 +652,45 @@ RT_FN f3 eval_texture(const KernelParams& P, int tex, float u, float v, f3 p) {
 }
 
 // rt_hit of a redirect target: parallelogram on (0, infinity) (Ray.hs:143-145)
-RT_FN bool target_hit(const DevTarget& T, f3 o, f3 d, float& t) {
+RT_FN bool target_hit(const DevTarget& T, f3 o, f3 d, real& t) {
   f3 n = ld3(T.n);
-  float denom = dot(n, d);
-  if (!(fabsf(denom) > 1e-8f)) return false;
+  real denom = dot(n, d);
+  if (!(RABS(denom) > RL(1e-8))) return false;
   f3 qo = ld3(T.q) - o;
   t = dot(n, qo) * RT_RCP(denom);
-  if (!(t > 0.0f)) return false;
+  if (!(t > RL(0.0))) return false;
   f3 prel = t * d - qo;
-  float a = dot(prel, ld3(T.wa)), b = dot(prel, ld3(T.wb));
-  return a >= 0.0f && a <= 1.0f && b >= 0.0f && b <= 1.0f;
+  real a = dot(prel, ld3(T.wa)), b = dot(prel, ld3(T.wb));
+  return a >= RL(0.0) && a <= RL(1.0) && b >= RL(0.0) && b <= RL(1.0);
 }
 
-// per-sample radiance -> 64-bit fixed point (2^-32); non-finite values set the pixel's flag
-RT_FN long long to_fixed(float x, bool& bad) {
-  if (!(fabsf(x) < 1.0e9f)) {
+// Per-sample radiance -> fixed point; non-finite values set the pixel's flag.  A lane sums the
+// samples of its item in an Acc and commits it with integer atomics (rt_kernel.hip).
+#if RT_F64
+// trunc(x 2^32) and the next 32 bits of x 2^64 (RT_ACC_WORDS = 6): x 2^32 and its floor are
+// exact in binary64 (a power-of-two scale), so is the fraction, and the fraction times 2^32 is
+// exact too, so the two words hold x to 2^-64 — every bit of a binary64 radiance >= 2^-11.
+struct Acc {
+  long long hi[3];
+  unsigned long long lo[3];
+};
+RT_FN void acc_add(Acc& A, int c, real x, bool& bad) {
+  if (!(RABS(x) < RL(1.0e9))) {
+    bad = true;
+    return;
+  }
+  const real xs = x * RL(4294967296.0);
+  const real fl = RFLOOR(xs);
+  A.hi[c] += (long long)fl;
+  A.lo[c] += (unsigned long long)(unsigned)((xs - fl) * RL(4294967296.0));
+}
+#else
+// trunc(x 2^32) (RT_ACC_WORDS = 3)
+struct Acc {
+  long long hi[3];
+};
+RT_FN long long to_fixed(real x, bool& bad) {
+  if (!(RABS(x) < RL(1.0e9))) {
     bad = true;
     return 0;
   }
@@ -551,10 +698,18 @@ RT_FN long long to_fixed(float x, bool& bad) {
   // in FP32 (x - floor(x) is exact) and the fraction scaled by 2^32 is exact, so two 32-bit
   // conversions give exactly trunc(x * 2^32).  (Negative inputs, possible only with negative
   // user colours, are within 2^-25 relative of it.)
-  const float fl = floorf(x);
+  const real fl = RFLOOR(x);
   const long long hi = (long long)(int)fl;
-  const unsigned lo = (unsigned)((x - fl) * 4294967296.0f);
+  const unsigned lo = (unsigned)((x - fl) * RL(4294967296.0));
   return (long long)((unsigned long long)hi << 32) + (long long)lo;
+}
+RT_FN void acc_add(Acc& A, int c, real x, bool& bad) { A.hi[c] += to_fixed(x, bad); }
+#endif
+RT_FN void acc_clear(Acc& A) { A = Acc{}; }
+RT_FN void acc_sample(Acc& A, f3 L, bool& bad) {
+  acc_add(A, 0, L.x, bad);
+  acc_add(A, 1, L.y, bad);
+  acc_add(A, 2, L.z, bad);
 }
 
 // ---------------------------------------------------------------- BVH traversal
@@ -562,10 +717,10 @@ RT_FN long long to_fixed(float x, bool& bad) {
 // rounds and continue in a later iteration of the lane loop with its state intact).
 struct TravState {
   int node, leaf, sp;
-  float tmin, tmin_up;
+  real tmin, tmin_up;
   Closest C;
 };
-RT_FN void trav_begin(TravState& S, int root, float tmin) {
+RT_FN void trav_begin(TravState& S, int root, real tmin) {
   S.node = root;
   S.leaf = 0;
   S.sp = 0;
@@ -591,48 +746,48 @@ RT_FN void trav_round(const KernelParams& P, const RayCtx& R, TravState& S, cons
   };
   while (S.node >= 0) {
     RT_COUNT(0);
-    v4 n0, n1, n2;
+    v4f n0, n1, n2;
     int cl, cr;
     const int node = S.node;
     if (node < P.lds_nodes) {  // top levels of the surface BVH, staged in LDS per workgroup
-      const v4* nd = W.lds_nodes + 4 * node;
+      const v4f* nd = W.lds_nodes + 4 * node;
       n0 = nd[0];
       n1 = nd[1];
       n2 = nd[2];
       cl = RT_F2I(nd[3].x);
       cr = RT_F2I(nd[3].y);
     } else {
-      cfp nd = cf(P.nodes) + 16 * (size_t)node;
-      n0 = ldc4(nd);
-      n1 = ldc4(nd + 4);
-      n2 = ldc4(nd + 8);
+      cfpf nd = (cfpf)P.nodes + 16 * (size_t)node;
+      n0 = ldc4f(nd);
+      n1 = ldc4f(nd + 4);
+      n2 = ldc4f(nd + 8);
       const RT_CAS i4* n3p = (const RT_CAS i4*)(nd + 12);
       cl = n3p->x;
       cr = n3p->y;
     }
-    float lx0 = fmaf(n0.x, R.idir.x, -R.oidir.x), lx1 = fmaf(n0.y, R.idir.x, -R.oidir.x);
-    float ly0 = fmaf(n0.z, R.idir.y, -R.oidir.y), ly1 = fmaf(n0.w, R.idir.y, -R.oidir.y);
-    float lz0 = fmaf(n2.x, R.idir.z, -R.oidir.z), lz1 = fmaf(n2.y, R.idir.z, -R.oidir.z);
-    float rx0 = fmaf(n1.x, R.idir.x, -R.oidir.x), rx1 = fmaf(n1.y, R.idir.x, -R.oidir.x);
-    float ry0 = fmaf(n1.z, R.idir.y, -R.oidir.y), ry1 = fmaf(n1.w, R.idir.y, -R.oidir.y);
-    float rz0 = fmaf(n2.z, R.idir.z, -R.oidir.z), rz1 = fmaf(n2.w, R.idir.z, -R.oidir.z);
-    float lnear = fmaxf(fmaxf(fminf(lx0, lx1), fminf(ly0, ly1)), fmaxf(fminf(lz0, lz1), S.tmin));
-    float lfar = fminf(fminf(fmaxf(lx0, lx1), fmaxf(ly0, ly1)), fminf(fmaxf(lz0, lz1), S.C.t));
-    float rnear = fmaxf(fmaxf(fminf(rx0, rx1), fminf(ry0, ry1)), fmaxf(fminf(rz0, rz1), S.tmin));
-    float rfar = fminf(fminf(fmaxf(rx0, rx1), fmaxf(ry0, ry1)), fminf(fmaxf(rz0, rz1), S.C.t));
+    real lx0 = RFMA(n0.x, R.idir.x, -R.oidir.x), lx1 = RFMA(n0.y, R.idir.x, -R.oidir.x);
+    real ly0 = RFMA(n0.z, R.idir.y, -R.oidir.y), ly1 = RFMA(n0.w, R.idir.y, -R.oidir.y);
+    real lz0 = RFMA(n2.x, R.idir.z, -R.oidir.z), lz1 = RFMA(n2.y, R.idir.z, -R.oidir.z);
+    real rx0 = RFMA(n1.x, R.idir.x, -R.oidir.x), rx1 = RFMA(n1.y, R.idir.x, -R.oidir.x);
+    real ry0 = RFMA(n1.z, R.idir.y, -R.oidir.y), ry1 = RFMA(n1.w, R.idir.y, -R.oidir.y);
+    real rz0 = RFMA(n2.z, R.idir.z, -R.oidir.z), rz1 = RFMA(n2.w, R.idir.z, -R.oidir.z);
+    real lnear = RMAX(RMAX(RMIN(lx0, lx1), RMIN(ly0, ly1)), RMAX(RMIN(lz0, lz1), S.tmin));
+    real lfar = RMIN(RMIN(RMAX(lx0, lx1), RMAX(ly0, ly1)), RMIN(RMAX(lz0, lz1), S.C.t));
+    real rnear = RMAX(RMAX(RMIN(rx0, rx1), RMIN(ry0, ry1)), RMAX(RMIN(rz0, rz1), S.tmin));
+    real rfar = RMIN(RMIN(RMAX(rx0, rx1), RMAX(ry0, ry1)), RMIN(RMAX(rz0, rz1), S.C.t));
 #ifdef RT_EXP_DOUBLE_NODE  // ablation: the slab tests computed twice (marginal cost of a node visit)
     {
-      const float e = (float)P.cam.pad;
-      float ax0 = fmaf(n0.x + e, R.idir.x, -R.oidir.x), ax1 = fmaf(n0.y + e, R.idir.x, -R.oidir.x);
-      float ay0 = fmaf(n0.z + e, R.idir.y, -R.oidir.y), ay1 = fmaf(n0.w + e, R.idir.y, -R.oidir.y);
-      float az0 = fmaf(n2.x + e, R.idir.z, -R.oidir.z), az1 = fmaf(n2.y + e, R.idir.z, -R.oidir.z);
-      float bx0 = fmaf(n1.x + e, R.idir.x, -R.oidir.x), bx1 = fmaf(n1.y + e, R.idir.x, -R.oidir.x);
-      float by0 = fmaf(n1.z + e, R.idir.y, -R.oidir.y), by1 = fmaf(n1.w + e, R.idir.y, -R.oidir.y);
-      float bz0 = fmaf(n2.z + e, R.idir.z, -R.oidir.z), bz1 = fmaf(n2.w + e, R.idir.z, -R.oidir.z);
-      lnear = fminf(lnear, fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fmaxf(fminf(az0, az1), S.tmin)));
-      lfar = fmaxf(lfar, fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fminf(fmaxf(az0, az1), S.C.t)));
-      rnear = fminf(rnear, fmaxf(fmaxf(fminf(bx0, bx1), fminf(by0, by1)), fmaxf(fminf(bz0, bz1), S.tmin)));
-      rfar = fmaxf(rfar, fminf(fminf(fmaxf(bx0, bx1), fmaxf(by0, by1)), fminf(fmaxf(bz0, bz1), S.C.t)));
+      const real e = (real)P.cam.pad;
+      real ax0 = RFMA(n0.x + e, R.idir.x, -R.oidir.x), ax1 = RFMA(n0.y + e, R.idir.x, -R.oidir.x);
+      real ay0 = RFMA(n0.z + e, R.idir.y, -R.oidir.y), ay1 = RFMA(n0.w + e, R.idir.y, -R.oidir.y);
+      real az0 = RFMA(n2.x + e, R.idir.z, -R.oidir.z), az1 = RFMA(n2.y + e, R.idir.z, -R.oidir.z);
+      real bx0 = RFMA(n1.x + e, R.idir.x, -R.oidir.x), bx1 = RFMA(n1.y + e, R.idir.x, -R.oidir.x);
+      real by0 = RFMA(n1.z + e, R.idir.y, -R.oidir.y), by1 = RFMA(n1.w + e, R.idir.y, -R.oidir.y);
+      real bz0 = RFMA(n2.z + e, R.idir.z, -R.oidir.z), bz1 = RFMA(n2.w + e, R.idir.z, -R.oidir.z);
+      lnear = RMIN(lnear, RMAX(RMAX(RMIN(ax0, ax1), RMIN(ay0, ay1)), RMAX(RMIN(az0, az1), S.tmin)));
+      lfar = RMAX(lfar, RMIN(RMIN(RMAX(ax0, ax1), RMAX(ay0, ay1)), RMIN(RMAX(az0, az1), S.C.t)));
+      rnear = RMIN(rnear, RMAX(RMAX(RMIN(bx0, bx1), RMIN(by0, by1)), RMAX(RMIN(bz0, bz1), S.tmin)));
+      rfar = RMAX(rfar, RMIN(RMIN(RMAX(bx0, bx1), RMAX(by0, by1)), RMIN(RMAX(bz0, bz1), S.C.t)));
     }
 #endif
     const bool hl = lnear <= lfar, hr = rnear <= rfar;
@@ -695,7 +850,7 @@ RT_FN void trav_round(const KernelParams& P, const RayCtx& R, TravState& S, cons
 #ifdef RT_EXP_DOUBLE_LEAF  // ablation: every leaf tested twice (marginal cost of the leaf tests)
     for (int k = 0; k < count; ++k)
       test_rec(P, ld_rec(cf(P.prims) + 16 * (size_t)(first + k)), first + k, R, S.tmin,
-               S.tmin_up + (float)P.cam.pad, S.C);
+               S.tmin_up + (real)P.cam.pad, S.C);
 #endif
     S.leaf = 0;
     if (S.node < 0 && S.node != kDone) {  // the node we stopped at is a leaf too: test it next
@@ -708,7 +863,7 @@ RT_FN void trav_round(const KernelParams& P, const RayCtx& R, TravState& S, cons
 // kFlat: the set is one flat leaf (rt_internal.h DevFlatSet); every lane walks the same
 // records in the same order, so the loops are coherent and the records are scalar loads.
 template <>
-RT_FN_SPEC void closest<true>(const KernelParams& P, cfp prims, int root, int set, const RayCtx& R, float tmin, Closest& C,
+RT_FN_SPEC void closest<true>(const KernelParams& P, cfp prims, int root, int set, const RayCtx& R, real tmin, Closest& C,
                          const Trav& W, int* overflow) {
   (void)prims;
   (void)root;
@@ -719,9 +874,9 @@ RT_FN_SPEC void closest<true>(const KernelParams& P, cfp prims, int root, int se
     const DevFlatSet& S = P.flat_sets[set];
 #ifdef RT_EXP_DOUBLE_TEST  // ablation: every flat set is tested twice (marginal cost of the tests)
     for (int rep = 0; rep < 2; ++rep) {
-    const float tmin_up = float_up(tmin) + (float)rep * P.cam.pad;
+    const real tmin_up = float_up(tmin) + (real)rep * P.cam.pad;
 #else
-    const float tmin_up = float_up(tmin);
+    const real tmin_up = float_up(tmin);
 #endif
     for (int b = S.box_first; b < S.box_end; ++b) test_box<true>((const RT_CAS DevBox*)P.boxes + b, R, tmin_up, C);
     int k = S.first;
@@ -733,17 +888,21 @@ RT_FN_SPEC void closest<true>(const KernelParams& P, cfp prims, int root, int se
 #ifdef RT_EXP_DOUBLE_TEST
     }
 #endif
+#if RT_F64
+    if (C.t < kInf) C.prim = C.ord;  // slot = primitive index (flat scenes store prims in slot order)
+#else
     const uint32_t hi = (uint32_t)(C.key >> 32);
     if (hi < 0x7f800000u) {  // a finite t won
-      C.t = __builtin_bit_cast(float, hi);
+      C.t = __builtin_bit_cast(real, hi);
       C.prim = (int)(uint32_t)C.key;  // slot = primitive index (flat scenes store prims in slot order)
     }
+#endif
   }
 }
 
 // BVH set (lockstep variant): resumable rounds run to completion.
 template <>
-RT_FN_SPEC void closest<false>(const KernelParams& P, cfp prims, int root, int set, const RayCtx& R, float tmin,
+RT_FN_SPEC void closest<false>(const KernelParams& P, cfp prims, int root, int set, const RayCtx& R, real tmin,
                           Closest& C, const Trav& W, int* overflow) {
   TravState S;
   trav_begin(S, root, tmin);
@@ -762,15 +921,15 @@ RT_FN void camera_ray(const KernelParams& P, uint32_t pix, int sample, int px, i
 #endif
   R.time = u01(w0.z);
   f3 origin = ld3(P.cam.center);
-  if (P.cam.disk_u[0] != 0.0f || P.cam.disk_u[1] != 0.0f || P.cam.disk_u[2] != 0.0f || P.cam.disk_v[0] != 0.0f ||
-      P.cam.disk_v[1] != 0.0f || P.cam.disk_v[2] != 0.0f) {
+  if (P.cam.disk_u[0] != RL(0.0) || P.cam.disk_u[1] != RL(0.0) || P.cam.disk_u[2] != RL(0.0) || P.cam.disk_v[0] != RL(0.0) ||
+      P.cam.disk_v[1] != RL(0.0) || P.cam.disk_v[2] != RL(0.0)) {
     u4 w1 = philox(pix, (uint32_t)sample, 0u, RT_EV_CAMERA1, P.key0, P.key1);
-    float rad = RT_SQRT(u01(w0.w)), s, c;
+    real rad = RT_SQRT(u01(w0.w)), s, c;
     RT_SINCOS_TURNS(u01(w1.x), &s, &c);
     origin = origin + (rad * c) * ld3(P.cam.disk_u) + (rad * s) * ld3(P.cam.disk_v);
   }
-  f3 target = ld3(P.cam.top_left) + ((float)px + u01(w0.x)) * ld3(P.cam.pixel_u) +
-              ((float)gy + u01(w0.y)) * ld3(P.cam.pixel_v);
+  f3 target = ld3(P.cam.top_left) + ((real)px + u01(w0.x)) * ld3(P.cam.pixel_u) +
+              ((real)gy + u01(w0.y)) * ld3(P.cam.pixel_v);
   R.o = origin;
   R.d = normalize(target - origin);
   R.self_gid = -1;
@@ -783,12 +942,12 @@ RT_FN void prep_ray(RayCtx& R) {
 
 // constantMedium's free-flight draw over the segment (lo, hi) (Geometry.hs:312-328); wm is the
 // Philox block of event RT_EV_MEDIA + m / 4 of this segment
-RT_FN void medium_draw(const KernelParams& P, int m, u4 wm, float lo, float hi, float& tbest, int& hit_medium) {
+RT_FN void medium_draw(const KernelParams& P, int m, u4 wm, real lo, real hi, real& tbest, int& hit_medium) {
   uint32_t wsel = (m & 3) == 0 ? wm.x : (m & 3) == 1 ? wm.y : (m & 3) == 2 ? wm.z : wm.w;
-  float rnd = 1.0f - u01(wsel);
-  float hit_dist = P.media[m].neg_inv_density * RT_LOG(rnd);
+  real rnd = RL(1.0) - u01(wsel);
+  real hit_dist = P.media[m].neg_inv_density * RT_LOG(rnd);
   if (hit_dist < hi - lo) {
-    float t = lo + hit_dist;
+    real t = lo + hit_dist;
     if (t < tbest) {
       tbest = t;
       hit_medium = m;
@@ -798,8 +957,8 @@ RT_FN void medium_draw(const KernelParams& P, int m, u4 wm, float lo, float hi, 
 RT_FN u4 medium_block(const KernelParams& P, int m, uint32_t pix, int sample, int seg) {
   return philox(pix, (uint32_t)sample, (uint32_t)seg, RT_EV_MEDIA + (uint32_t)(m >> 2), P.key0, P.key1);
 }
-RT_FN void medium_event(const KernelParams& P, int m, uint32_t pix, int sample, int seg, float lo, float hi,
-                        float& tbest, int& hit_medium) {
+RT_FN void medium_event(const KernelParams& P, int m, uint32_t pix, int sample, int seg, real lo, real hi,
+                        real& tbest, int& hit_medium) {
   medium_draw(P, m, medium_block(P, m, pix, sample, seg), lo, hi, tbest, hit_medium);
 }
 
@@ -809,15 +968,15 @@ RT_FN void medium_event(const KernelParams& P, int m, uint32_t pix, int sample, 
 // kMats: the scene has materials beyond lightSource / pitchBlack / lambertian; their code is
 // compiled only into those instantiations (the Cornell box and the bunny have none: -2.4 % / -1.2 %)
 template <int kTex, bool kMats>
-RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int& seg, float tbest, int best,
+RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int& seg, real tbest, int best,
                  int hit_medium, RayCtx& R, f3& L, f3& T) {
   RT_HOOK_SEGMENT(pix, sample, seg, R, tbest, best, hit_medium, L, T);
   if (hit_medium < 0 && best < 0) {
     // miss: cs_background (Ray.hs:179)
     f3 bg = ld3(P.cam.bg0);
     if (P.cam.bg_kind == 1) {
-      float a = 0.5f * (R.d.y + 1.0f);
-      bg = (1.0f - a) * bg + a * ld3(P.cam.bg1);
+      real a = RL(0.5) * (R.d.y + RL(1.0));
+      bg = (RL(1.0) - a) * bg + a * ld3(P.cam.bg1);
     }
     L = L + T * bg;
     return true;
@@ -827,7 +986,7 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
   const RT_CAS DevMaterial* Mp = hit_medium >= 0
                                      ? (const RT_CAS DevMaterial*)P.mats + P.media[hit_medium].material
                                      : (const RT_CAS DevMaterial*)P.prim_shade + best;
-  const DevMaterial Mt = DevMaterial{Mp->kind, Mp->tex, Mp->param, Mp->tex_const, {0.f, 0.f, 0.f}, 0.f};
+  const DevMaterial Mt = DevMaterial{Mp->kind, Mp->tex, Mp->param, Mp->tex_const, {RL(0.), RL(0.), RL(0.)}, RL(0.)};
   // every material but pitchBlack and dielectric reads its texture; constant textures come with
   // the record, the others are evaluated once (one inlined copy keeps the register allocation down)
   // (kTex: 0 — every texture is constant, the texture code is not compiled in; 1 — uv / image
@@ -838,8 +997,8 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
     h.p = R.o + tbest * R.d;
     h.n = -R.d;
     h.front = true;
-    h.u = 0.f;
-    h.v = 0.f;
+    h.u = RL(0.);
+    h.v = RL(0.);
     h.gid = -1;
   } else {
     h = surface_info(P, prims, best, R, tbest, need_tex);
@@ -865,7 +1024,7 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
     case 5: {  // metal
       if constexpr (!kMats) break;
       f3 d2 = reflect(h.n, R.d) + Mt.param * unit_vector(w.y, w.z);
-      if (dot(d2, h.n) > 0.0f) {
+      if (dot(d2, h.n) > RL(0.0)) {
         T = T * tex;
         newdir = normalize(d2);
       } else {
@@ -875,19 +1034,19 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
     }
     case 6: {  // dielectric
       if constexpr (!kMats) break;
-      float ior = Mt.param;
-      float ratio = h.front ? RT_RCP(ior) : ior;
-      float cos_t = fminf(1.0f, -dot(h.n, R.d));
-      float sin_t = RT_SQRT(fmaxf(0.0f, 1.0f - cos_t * cos_t));
-      float r0 = (1.0f - ratio) * RT_RCP(1.0f + ratio);
+      real ior = Mt.param;
+      real ratio = h.front ? RT_RCP(ior) : ior;
+      real cos_t = RMIN(RL(1.0), -dot(h.n, R.d));
+      real sin_t = RT_SQRT(RMAX(RL(0.0), RL(1.0) - cos_t * cos_t));
+      real r0 = (RL(1.0) - ratio) * RT_RCP(RL(1.0) + ratio);
       r0 = r0 * r0;
-      float x1 = 1.0f - cos_t, x2 = x1 * x1;
-      float reflectance = r0 + (1.0f - r0) * (x2 * x2 * x1);
-      if (ratio * sin_t > 1.0f || u01(w.x) < reflectance) {
+      real x1 = RL(1.0) - cos_t, x2 = x1 * x1;
+      real reflectance = r0 + (RL(1.0) - r0) * (x2 * x2 * x1);
+      if (ratio * sin_t > RL(1.0) || u01(w.x) < reflectance) {
         newdir = unit(reflect(h.n, R.d));
       } else {
         f3 perp = ratio * (R.d + cos_t * h.n);
-        newdir = unit(perp - RT_SQRT(fabsf(1.0f - dot(perp, perp))) * h.n);
+        newdir = unit(perp - RT_SQRT(RABS(RL(1.0) - dot(perp, perp))) * h.n);
       }
       break;
     }
@@ -897,7 +1056,7 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
       break;
     default: {  // 2 lambertian, 3 lommelSeeliger (HemisphereF); 8 isotropic, 9 anisotropic (SphereF)
       const bool hemi = !kMats || Mt.kind == 2 || Mt.kind == 3;
-      float cr = u01(w.x);
+      real cr = u01(w.x);
       int choice = -1;
       for (int k = 0; k < P.n_targets; ++k) {
         if (cr < P.targets[k].thresh) {
@@ -914,27 +1073,27 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
         f3 lp = ld3(Tg.q) + u01(w.y) * ld3(Tg.u) + u01(w.z) * ld3(Tg.v);
         dir = normalize(lp - h.p);
       }
-      float pdf1 = hemi ? dot(dir, h.n) * (1.0f / kPi) : 0.25f / kPi;
-      if (hemi && pdf1 <= 0.0f) {
+      real pdf1 = hemi ? dot(dir, h.n) * (RL(1.0) / kPi) : RL(0.25) / kPi;
+      if (hemi && pdf1 <= RL(0.0)) {
         terminate = true;
         break;
       }
-      float mix = 0.0f;
+      real mix = RL(0.0);
       for (int k = 0; k < P.n_targets; ++k) {
-        float tt;
+        real tt;
         if (target_hit(P.targets[k], h.p, dir, tt))
-          mix += P.targets[k].prob * (tt * tt * RT_RCP(fabsf(dot(ld3(P.targets[k].cr), dir))));
+          mix += P.targets[k].prob * (tt * tt * RT_RCP(RABS(dot(ld3(P.targets[k].cr), dir))));
       }
-      float pdf = P.rem_prob * pdf1 + mix;
+      real pdf = P.rem_prob * pdf1 + mix;
       f3 f = tex;
       if (!kMats) {
       } else if (Mt.kind == 3) {
-        float mu0 = -dot(R.d, h.n), mu1 = dot(dir, h.n);
-        f = (0.25f * RT_RCP(mu0 + mu1)) * f;
+        real mu0 = -dot(R.d, h.n), mu1 = dot(dir, h.n);
+        f = (RL(0.25) * RT_RCP(mu0 + mu1)) * f;
       } else if (Mt.kind == 9) {
-        float g = Mt.param, mu = dot(R.d, dir);
-        float base = 1.0f + g * g - 2.0f * g * mu;
-        f = ((1.0f - g * g) * RT_RCP(base * RT_SQRT(base))) * f;
+        real g = Mt.param, mu = dot(R.d, dir);
+        real base = RL(1.0) + g * g - RL(2.0) * g * mu;
+        f = ((RL(1.0) - g * g) * RT_RCP(base * RT_SQRT(base))) * f;
       }
       T = T * ((pdf1 * RT_RCP(pdf)) * f);
       newdir = dir;
@@ -983,39 +1142,40 @@ RT_FN bool open_item(const KernelParams& P, int item, ItemCtx& I) {
 }
 
 // The lockstep persistent lane loop.  `grab(need)` is wave-collective: it returns a fresh item
-// for lanes with need == true.  `commit(tile_pixel, sx, sy, sz, bad)` adds a finished item's
+// for lanes with need == true.  `commit(tile_pixel, acc, bad)` adds a finished item's
 // sums.  One segment per iteration, all of its queries run by the whole wave together: the flat
 // kernel (every lane tests the same primitives), and the lockstep BVH variant kept for
 // experiments (RT_VAR_BVH_LOCKSTEP; BVH scenes, media or not, default to lane_loop_bvh).
 template <bool kFlat, int kTex, bool kMedia, bool kMats, class Grab, class Commit>
 RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW,
-                             const float* prims_) {
+                             const real* prims_) {
   const cfp prims = cf(prims_);
   int overflow = 0;
   ItemCtx I{-1, 0, 0, 0, 0, 0, 0u};
   int seg = 0;
-  long long sx = 0, sy = 0, sz = 0;
+  Acc acc;
+  acc_clear(acc);
   bool bad = false;
   bool alive = false;
-  f3 L = mk3(0.f, 0.f, 0.f), T = mk3(1.f, 1.f, 1.f);
+  f3 L = mk3(RL(0.), RL(0.), RL(0.)), T = mk3(RL(1.), RL(1.), RL(1.));
   RayCtx R;
   R.o = R.d = R.idir = R.oidir = L;
-  R.time = 0.0f;
+  R.time = RL(0.0);
   R.self_gid = -1;
   for (;;) {
     const bool need = !alive && I.sample >= I.s_end;
-    if (need && I.item >= 0) commit(I.tp, sx, sy, sz, bad);
+    if (need && I.item >= 0) commit(I.tp, acc, bad);
     const int got = grab(need);
     if (need) {
       if (got >= P.n_items) break;
-      sx = sy = sz = 0;
+      acc_clear(acc);
       bad = false;
       if (!open_item(P, got, I)) continue;
     }
     if (!alive) {
       camera_ray(P, I.pix, I.sample, I.px, I.gy, R);
-      L = mk3(0.f, 0.f, 0.f);
-      T = mk3(1.f, 1.f, 1.f);
+      L = mk3(RL(0.), RL(0.), RL(0.));
+      T = mk3(RL(1.), RL(1.), RL(1.));
       seg = 0;
       alive = true;
     }
@@ -1024,7 +1184,7 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
     if constexpr (!kFlat) prep_ray(R);  // reciprocal direction: BVH slab tests only
     Closest C = no_hit();
     closest<kFlat>(P, prims, P.surface_root, 0, R, kTmin, C, TW, &overflow);
-    float tbest = C.t;
+    real tbest = C.t;
     const int best = C.prim;
     int hit_medium = -1;
     // media: compiled only into the instantiations for scenes that have them (kMedia)
@@ -1040,8 +1200,8 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
         closest<kFlat>(P, prims, M.root, m + 1, R, kTmin, C1, TW, &overflow);
       }
       if (C1.prim < 0) continue;
-      const float t1 = C1.t;
-      float lo, hi;
+      const real t1 = C1.t;
+      real lo, hi;
       if (prim_front(P, prims, C1.prim, R, t1)) {
         if (!(t1 < tbest)) continue;
         Closest C2 = no_hit();
@@ -1057,9 +1217,7 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
     }
     if (shade<kTex, kMats>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T)) {
       RT_HOOK_SAMPLE(I.pix, I.sample, L);
-      sx += to_fixed(L.x, bad);
-      sy += to_fixed(L.y, bad);
-      sz += to_fixed(L.z, bad);
+      acc_sample(acc, L, bad);
       alive = false;
       ++I.sample;
     }
@@ -1079,40 +1237,41 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
 // soon as the previous one finishes.
 enum : int { ST_NEED_ITEM = 0, ST_NEED_SAMPLE = 1, ST_START_SEG = 2, ST_TRACE = 3, ST_SHADE = 4 };
 template <int kTex, bool kMedia, bool kMats, class Grab, class Commit>
-RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW, const float* prims_) {
+RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW, const real* prims_) {
   const cfp prims = cf(prims_);
   const int n_media = kMedia ? P.n_media : 0;  // media code only in the kMedia instantiations
   int overflow = 0;
   ItemCtx I{-1, 0, 0, 0, 0, 0, 0u};
   int seg = 0;
-  long long sx = 0, sy = 0, sz = 0;
+  Acc acc;
+  acc_clear(acc);
   bool bad = false;
   int state = ST_NEED_ITEM;
-  f3 L = mk3(0.f, 0.f, 0.f), T = mk3(1.f, 1.f, 1.f);
+  f3 L = mk3(RL(0.), RL(0.), RL(0.)), T = mk3(RL(1.), RL(1.), RL(1.));
   RayCtx R;
   R.o = R.d = R.idir = R.oidir = L;
-  R.time = 0.0f;
+  R.time = RL(0.0);
   R.self_gid = -1;
   TravState S;
   trav_begin(S, RT_EMPTY_ROOT, kTmin);
   // query sequencing within a segment: q = 0 surfaces; q = 1 + 2m / 2 + 2m medium m, 1st / 2nd hit
   int q = 0, best = -1, hit_medium = -1;
-  float tbest = kInf, t1 = 0.0f, t_surf = kInf;
+  real tbest = kInf, t1 = RL(0.0), t_surf = kInf;
   for (;;) {
     // ---- front end: items, samples, segment starts (lanes not tracing)
     const bool need = state == ST_NEED_ITEM;
-    if (need && I.item >= 0) commit(I.tp, sx, sy, sz, bad);
+    if (need && I.item >= 0) commit(I.tp, acc, bad);
     const int got = grab(need);
     if (need) {
       if (got >= P.n_items) break;
-      sx = sy = sz = 0;
+      acc_clear(acc);
       bad = false;
       state = open_item(P, got, I) ? ST_NEED_SAMPLE : ST_NEED_ITEM;
     }
     if (state == ST_NEED_SAMPLE) {
       camera_ray(P, I.pix, I.sample, I.px, I.gy, R);
-      L = mk3(0.f, 0.f, 0.f);
-      T = mk3(1.f, 1.f, 1.f);
+      L = mk3(RL(0.), RL(0.), RL(0.));
+      T = mk3(RL(1.), RL(1.), RL(1.));
       seg = 0;
       state = ST_START_SEG;
     }
@@ -1186,9 +1345,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
     if (state == ST_SHADE) {
       if (shade<kTex, kMats>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T)) {
         RT_HOOK_SAMPLE(I.pix, I.sample, L);
-        sx += to_fixed(L.x, bad);
-        sy += to_fixed(L.y, bad);
-        sz += to_fixed(L.z, bad);
+        acc_sample(acc, L, bad);
         ++I.sample;
         state = I.sample < I.s_end ? ST_NEED_SAMPLE : ST_NEED_ITEM;
       } else {
@@ -1199,4 +1356,4 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
   return overflow;
 }
 
-}  // namespace rtk
+}  // namespace RT_NS

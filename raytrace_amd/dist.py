@@ -19,7 +19,8 @@ from .ray import DeviceScene, assemble_shards, shard_rows
 
 
 class ShardedRenderer:
-    def __init__(self, settings: CameraSettings, world, row_block: int = 4, device=None, tile_fn=None, group=None):
+    def __init__(self, settings: CameraSettings, world, row_block: int = 4, device=None, tile_fn=None, group=None,
+                 precision: str = "f64"):
         import torch
         import torch.distributed as dist
         self.torch = torch
@@ -33,6 +34,8 @@ class ShardedRenderer:
         self.w = int(settings.cs_imageWidth)
         self.rows = shard_rows(self.h, self.world_size, row_block)
         self.tile_fn = tile_fn
+        self.precision = precision
+        dtype = torch.float64 if precision == "f64" else torch.float32
         if tile_fn is None:
             self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
             self.scene = DeviceScene(world, device=self.device.index or 0)
@@ -40,18 +43,19 @@ class ShardedRenderer:
             self.device = torch.device("cpu")
             self.scene = None
             self.world = world
-        self.tile = torch.empty((self.rows, self.w, 3), dtype=torch.float32, device=self.device)
-        self.gathered = torch.empty((self.world_size * self.rows, self.w, 3), dtype=torch.float32, device=self.device)
+        self.tile = torch.empty((self.rows, self.w, 3), dtype=dtype, device=self.device)
+        self.gathered = torch.empty((self.world_size * self.rows, self.w, 3), dtype=dtype, device=self.device)
 
     def render_tile(self, seed, stream=None):
         """Enqueue (GPU) or compute (tile_fn) this rank's rows into self.tile."""
         if self.tile_fn is not None:
             self.tile.copy_(self.torch.from_numpy(np.ascontiguousarray(
-                self.tile_fn(self.settings, self.world, seed, self.world_size, self.rank, self.row_block))))
+                self.tile_fn(self.settings, self.world, seed, self.world_size, self.rank, self.row_block))).to(
+                self.tile.dtype))
             return
         s = stream if stream is not None else self.torch.cuda.current_stream(self.device)
         self.scene.render_async(self.settings, seed, self.tile.data_ptr(), s.cuda_stream, n_shards=self.world_size,
-                                shard=self.rank, row_block=self.row_block)
+                                shard=self.rank, row_block=self.row_block, precision=self.precision)
 
     def gather(self):
         if self.world_size > 1:

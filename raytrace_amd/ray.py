@@ -30,13 +30,18 @@ def _seed64(seed) -> int:
     raise TypeError("seed must be a StdGen (mkStdGen n) or an int")
 
 
-def raytrace(settings: CameraSettings, world, seed, device: int = 0, stats: dict | None = None) -> np.ndarray:
-    """Render on the GPU.  Returns float32 (height, width, 3), linear RGB."""
+def raytrace(settings: CameraSettings, world, seed, device: int = 0, stats: dict | None = None,
+             precision: str = "f64", devices=None, row_block: int = 4) -> np.ndarray:
+    """Render on the GPU.  Returns (height, width, 3) linear RGB: float64 computed in binary64 as the
+    reference does (default), or float32 from the FP32 kernel (precision="f32").  `devices`: a list
+    of HIP devices that render the image together from this process (rt_exec device list; rows
+    dealt round-robin in blocks of `row_block`); the image is identical to the one-device render."""
     L = _lib.load()
     flat = world if isinstance(world, FlatScene) else flatten(world)
     cs = _lib.camera_struct(settings)
     sc = _lib.scene_struct(flat)
-    ex = _lib.exec_struct(device=device)
+    ex = _lib.exec_struct(device=device, precision=precision, devices=devices,
+                          row_block=row_block if devices else 4)
     h = image_height(settings)
     w = int(settings.cs_imageWidth)
     if h <= 0 or w <= 0:
@@ -45,7 +50,7 @@ def raytrace(settings: CameraSettings, world, seed, device: int = 0, stats: dict
     rows = _lib.check(L.rt_shard_rows(h, ctypes.byref(ex)))
     if rows != h:
         raise RuntimeError(f"librt_amd.so reports {rows} rows for a {h}-row image")
-    out = np.zeros((h, w, 3), np.float32)
+    out = np.zeros((h, w, 3), _lib.dtype_of(precision))
     st = _lib.RtStats()
     _lib.check(L.rt_render(ctypes.byref(cs), ctypes.byref(sc), _seed64(seed), ctypes.byref(ex),
                            out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st)))
@@ -56,15 +61,15 @@ def raytrace(settings: CameraSettings, world, seed, device: int = 0, stats: dict
 
 
 def render_shard(settings: CameraSettings, world, seed, n_shards: int, shard: int, row_block: int = 4,
-                 device: int = 0) -> np.ndarray:
+                 device: int = 0, precision: str = "f64") -> np.ndarray:
     """Render only the rows of one shard (rt_exec row interleave); returns (rows, width, 3)."""
     L = _lib.load()
     flat = world if isinstance(world, FlatScene) else flatten(world)
     cs = _lib.camera_struct(settings)
     sc = _lib.scene_struct(flat)
-    ex = _lib.exec_struct(device=device, n_shards=n_shards, shard=shard, row_block=row_block)
+    ex = _lib.exec_struct(device=device, n_shards=n_shards, shard=shard, row_block=row_block, precision=precision)
     rows = _lib.check(L.rt_shard_rows(image_height(settings), ctypes.byref(ex)))
-    out = np.zeros((rows, int(settings.cs_imageWidth), 3), np.float32)
+    out = np.zeros((rows, int(settings.cs_imageWidth), 3), _lib.dtype_of(precision))
     st = _lib.RtStats()
     _lib.check(L.rt_render(ctypes.byref(cs), ctypes.byref(sc), _seed64(seed), ctypes.byref(ex),
                            out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st)))
@@ -115,10 +120,12 @@ class DeviceScene:
         return dict(upload_ms=st.upload_ms, bvh_nodes=st.bvh_nodes, max_stack=st.max_stack)
 
     def render_async(self, settings: CameraSettings, seed, out_ptr: int, stream_ptr: int = 0, n_shards: int = 1,
-                     shard: int = 0, row_block: int = 4):
-        """Enqueue a render into the device buffer at out_ptr (rows x width x 3 float32)."""
+                     shard: int = 0, row_block: int = 4, precision: str = "f64"):
+        """Enqueue a render into the device buffer at out_ptr (rows x width x 3 float64, or float32
+        with precision="f32")."""
         cs = _lib.camera_struct(settings)
-        ex = _lib.exec_struct(device=self.device, n_shards=n_shards, shard=shard, row_block=row_block)
+        ex = _lib.exec_struct(device=self.device, n_shards=n_shards, shard=shard, row_block=row_block,
+                              precision=precision)
         _lib.check(self._lib.rt_render_async(self.handle, ctypes.byref(cs), _seed64(seed), ctypes.byref(ex),
                                              ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream_ptr or None)))
 
@@ -138,8 +145,10 @@ class DeviceScene:
 
 def encode8(rgb: np.ndarray, encoding: str = "srgb") -> np.ndarray:
     """8-bit codes as the reference's writers store them: min(255, floor(256 * transfer(clamp01 x)))
-    with transfer = sRGB (writeImage) or sqrt (writeImageSqrt).  Host twin of rt_encode8_async."""
-    x = np.clip(np.asarray(rgb, np.float64), 0.0, 1.0)
+    with transfer = sRGB (writeImage) or sqrt (writeImageSqrt); NaN -> 0.  Host twin of
+    rt_encode8_async (which is bit-exact against it)."""
+    x = np.asarray(rgb, np.float64)
+    x = np.clip(np.where(np.isnan(x), 0.0, x), 0.0, 1.0)
     if encoding == "sqrt":
         t = np.sqrt(x)
     else:

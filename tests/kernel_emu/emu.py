@@ -23,7 +23,8 @@ def lib():
     return _lib
 
 
-def render(settings, world, seed, n_shards=1, shard=0, row_block=4, nthreads=None, chunk=0, counters=False):
+def render(settings, world, seed, n_shards=1, shard=0, row_block=4, nthreads=None, chunk=0, counters=False,
+           precision="f64"):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
     from raytrace_amd import _lib as R
@@ -36,12 +37,13 @@ def render(settings, world, seed, n_shards=1, shard=0, row_block=4, nthreads=Non
     ex = R.exec_struct(0, n_shards, shard, row_block)
     h = image_height(settings)
     rows = shard_rows(h, n_shards, row_block)
-    out = np.zeros((rows, int(settings.cs_imageWidth), 3), np.float32)
+    out = np.zeros((rows, int(settings.cs_imageWidth), 3), np.float64 if precision == "f64" else np.float32)
     L = lib()
     cnt = np.zeros(4, np.int64)
     rc = L.rt_emu_render(ctypes.byref(cs), ctypes.byref(sc), ctypes.c_uint64(_seed64(seed)), ctypes.byref(ex),
                          out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(nthreads or min(16, os.cpu_count() or 1)),
-                         ctypes.c_int(chunk), cnt.ctypes.data_as(ctypes.c_void_p))
+                         ctypes.c_int(chunk), cnt.ctypes.data_as(ctypes.c_void_p),
+                         ctypes.c_int(1 if precision == "f64" else 0))
     if rc != 0:
         raise RuntimeError(f"rt_emu_render failed {rc}: {L.rt_emu_last_error().decode()}")
     if counters:

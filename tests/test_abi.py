@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
     exported = set(re.findall(r"\bT (rt_\w+)", out.stdout))
     assert set(names) <= exported
-    assert L.rt_abi_version() == 2
+    assert L.rt_abi_version() == _lib.ABI_VERSION == 3
 
 
 def test_host_only_entry_points_without_gpu():
@@ -63,7 +63,7 @@ int main(void) {
   P(rt_perlin); O(rt_perlin, grad);
   P(rt_camera_settings); O(rt_camera_settings, image_width); O(rt_camera_settings, background_c0);
   O(rt_camera_settings, defocus_angle); O(rt_camera_settings, redirect_targets);
-  P(rt_redirect_target); P(rt_exec); P(rt_stats); O(rt_stats, samples);
+  P(rt_redirect_target); P(rt_exec); O(rt_exec, flags); O(rt_exec, devices); P(rt_stats); O(rt_stats, samples);
   return 0;
 }
 """
@@ -96,6 +96,7 @@ def test_record_layouts_match_header():
         assert c[f"rt_camera_settings.{f}"] == getattr(_lib.RtCameraSettings, f).offset, f
     assert c["rt_redirect_target"] == ctypes.sizeof(_lib.RtRedirectTarget)
     assert c["rt_exec"] == ctypes.sizeof(_lib.RtExec)
+    assert c["rt_exec.flags"] == _lib.RtExec.flags.offset and c["rt_exec.devices"] == _lib.RtExec.devices.offset
     assert c["rt_stats"] == ctypes.sizeof(_lib.RtStats) and c["rt_stats.samples"] == _lib.RtStats.samples.offset
 
 
@@ -125,3 +126,25 @@ def test_scene_validation_errors_before_device():
         R.raytrace(cs.replace(cs_aspectRatio=0.0), world, seed)
     with pytest.raises(R.RtUnsupported):
         R.raytrace(cs.replace(cs_redirectTargets=[(0.01, (0, 0, 0), (1, 0, 0), (0, 1, 0))] * 9), world, seed)
+    with pytest.raises(ValueError):
+        R.raytrace(cs, world, seed, precision="f16")
+
+
+def test_device_list_validation_before_device():
+    """ABI v3 device lists: malformed lists are RT_E_INVALID before any device is touched."""
+    import pytest
+    from raytrace_amd import scenes
+    L = _lib.load()
+    cs, world, seed = scenes.cornell_box(spp=1, width=4)
+    from raytrace_amd.scene import flatten
+    c, sc = _lib.camera_struct(cs), _lib.scene_struct(flatten(world))
+    out = np.zeros((4, 4, 3))
+    ex = _lib.exec_struct(devices=[0, 0])
+    ex.n_shards = 2  # a device list renders the whole image
+    assert L.rt_render(ctypes.byref(c), ctypes.byref(sc), 1, ctypes.byref(ex), out.ctypes.data, None) == _lib.RT_E_INVALID
+    assert b"n_shards" in L.rt_last_error()
+    ex = _lib.exec_struct(devices=[0])
+    ex.n_devices = 65
+    assert L.rt_render(ctypes.byref(c), ctypes.byref(sc), 1, ctypes.byref(ex), out.ctypes.data, None) == _lib.RT_E_INVALID
+    with pytest.raises(ValueError):
+        _lib.exec_struct(precision="bf16")
