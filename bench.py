@@ -20,15 +20,22 @@ default for them): a frame's last long paths occupy few CUs, and the next frame'
 workgroups fill the rest instead of waiting (Cornell +4 % at 1 GPU, +26 % on one rank's share of
 an 8-GPU frame).
 
-Extra fields: `roofline` (the render kernel's SURVEY.md §8(d) algorithmic bytes per launch /
-its device time per frame, from HIP events over the timed region — `kernel_ms`, the span of the
-timed frames / frames; `launch_ms` is the average single-launch duration, longer because two
-launches overlap — vs the 8 TB/s HBM peak; `traffic` = PMC-measured HBM bytes per
-launch from the committed rocprofv3 summary, when present), `issue_roofline` (the kernel's
-PMC-counted VALU wave-instructions per launch / its time vs the chip's VALU issue ceiling — the
-physical limiter of this cache-resident, branchy FP32 kernel) and `cpu_baseline`
-(the FP64 oracle, the CPU restatement of the reference's algorithm, on a bounded row sample,
-rank 0 at N=1 only, with a 1-core figure beside the threaded one).
+Precision: the line is measured with the binary64 kernel (`dtype` "f64"), the reference's
+arithmetic (`V3 Double`, Core.hs:29-31); the FP32 fast path is measured right after it on the
+same frames and reported beside it as `f32_fast_path` (a labelled second record, not `value`).
+
+Extra fields: `roofline` — the physical ceiling of the render kernel: VALU instruction issue
+(the kernel's PMC-counted VALU wave-instructions per launch, profiles/pmc_valu.json, scaled to the
+samples this launch renders, / its device time per frame from HIP events over the timed region —
+`kernel_ms`, the span of the timed frames / frames; `launch_ms` is the average single-launch
+duration, longer when two launches overlap — against 256 CUs x 4 SIMDs x one wave64 VALU
+instruction per 2 cycles at 2.4 GHz; frac <= 1 by construction), with `traffic` = the PMC-measured
+HBM bytes per launch and `hbm_gbs` = traffic / kernel time beside it, and the SURVEY.md §8(d)
+algorithmic bytes (the REFERENCE's traversal: every Cornell quad tested every segment) kept as a
+labelled `reference_traversal_bytes` figure — it exceeds HBM peak because the kernel reads its
+1.4 KB scene from the scalar cache, so it is never `frac`; `cpu_baseline` — the FP64 oracle, the
+CPU restatement of the reference's algorithm, on a bounded row sample, rank 0 at N=1 only, on
+every core this process may use (os.sched_getaffinity), with a 1-core figure beside it.
 """
 import argparse
 import json
@@ -48,8 +55,30 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def host_cpu_info():
+    """CPU model, the machine's CPUs, the CPUs this process may run on and the cgroup CPU quota."""
+    info = {"host_cpus": os.cpu_count()}
+    try:
+        info["usable_cpus"] = len(os.sched_getaffinity(0))
+    except Exception:
+        info["usable_cpus"] = os.cpu_count()
+    try:
+        with open("/proc/cpuinfo") as f:
+            info["cpu_model"] = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except Exception:
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        pass
+    return info
+
+
 def cpu_baseline(config, world_fn, row_stride=6):
-    """Time the oracle (binary64 restatement, splitmix draw order) on every `row_stride`-th row."""
+    """Time the oracle (binary64 restatement, splitmix draw order) on every `row_stride`-th row, on
+    every CPU this process may run on (the reference's `-threaded -N`: one capability per core)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle
@@ -58,7 +87,10 @@ def cpu_baseline(config, world_fn, row_stride=6):
     h, w = image_height(cs), cs.cs_imageWidth
     rows = np.arange(0, h, row_stride)
     pix = (rows[:, None] * w + np.arange(w)[None, :]).reshape(-1).astype(np.int32)
-    threads = min(16, os.cpu_count() or 1)
+    hw = host_cpu_info()
+    threads = max(1, hw["usable_cpus"] or 1)
+    if hw.get("cgroup_cpu_quota"):  # more threads than the CPU quota only time-share it
+        threads = max(1, min(threads, int(round(hw["cgroup_cpu_quota"]))))
     oracle.render(cs, world, seed, mode=oracle.RNG_SPLITMIX, pixels=pix[:64], nthreads=threads)  # warm
     t0 = time.perf_counter()
     oracle.render(cs, world, seed, mode=oracle.RNG_SPLITMIX, pixels=pix, nthreads=threads)
@@ -71,24 +103,11 @@ def cpu_baseline(config, world_fn, row_stride=6):
     dt1 = time.perf_counter() - t0
     samples1 = len(pix1) * cs.cs_samplesPerPixel
     return {"value": round(samples / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "value_1core": round(samples1 / dt1 / 1e6, 4), "host_cpus": os.cpu_count(),
+            "value_1core": round(samples1 / dt1 / 1e6, 4), **hw,
             "sample": f"{config}: every {row_stride}th row ({len(rows)} rows x {w} px x {cs.cs_samplesPerPixel} spp"
                       f" = {samples / 1e6:.1f} M samples) in {dt:.2f} s, oracle/rt_oracle.c splitmix mode, "
                       f"{threads} threads; 1-core: every {10 * row_stride}th row ({samples1 / 1e6:.2f} M samples)"
                       f" in {dt1:.2f} s"}
-
-
-def pmc_traffic(config):
-    """HBM bytes per launch of the render kernel from the committed rocprofv3 PMC summary."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
-        return None
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        return d.get(config, {}).get("hbm_bytes_per_launch")
-    except Exception:
-        return None
 
 
 # VALU issue ceiling: 256 CUs x 4 SIMD-32 x one wave64 VALU instruction per 2 cycles at the
@@ -96,18 +115,45 @@ def pmc_traffic(config):
 VALU_PEAK_GINST = 256 * 4 * 0.5 * 2.4
 
 
-def pmc_valu(config, kernel_ms):
-    """Issue roofline of the render kernel from the committed PMC VALU counts (profiles/pmc_valu.json)."""
+def pmc_record(config, precision):
+    """The committed PMC summary of the render kernel for (config, precision) (profiles/pmc_valu.json)."""
     path = os.path.join(ROOT, "profiles", "pmc_valu.json")
     try:
         with open(path) as f:
-            d = json.load(f)[config]
+            d = json.load(f)
     except Exception:
         return None
-    ach = d["valu_insts_per_launch"] / (kernel_ms * 1e-3) / 1e9
-    return {"bound": "valu-issue", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
-            "frac": round(ach / VALU_PEAK_GINST, 4), "lane_utilisation": round(d["lane_utilisation"], 4),
-            "valu_insts_per_launch": d["valu_insts_per_launch"], "pmc_round": d.get("round")}
+    return d.get(f"{config}/{precision}")
+
+
+def roofline_of(config, precision, kernel_ms, launch_ms, share, samples_per_launch, concurrent):
+    """The physical roofline of the render kernel: VALU issue from the committed PMC counts (full
+    frame, scaled by `share` = the fraction of the frame's samples this launch renders), measured
+    HBM traffic beside it, and the reference-traversal bytes as a labelled figure."""
+    with open(os.path.join(ROOT, "tests", "golden", "algbytes.json")) as f:
+        b_sample = json.load(f)["configs"][config]["bytes_per_sample"]
+    ref_bytes = b_sample * samples_per_launch
+    r = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_GINST, "unit": "G VALU wave-instr/s", "frac": None,
+         "traffic": None, "kernel": "rt_render_kernel", "precision": precision, "kernel_ms": round(kernel_ms, 4),
+         "launch_ms": round(launch_ms, 4), "concurrent_launches": concurrent,
+         "samples_per_launch": samples_per_launch,
+         "reference_traversal_bytes": {"bytes_per_sample": round(b_sample, 1), "per_launch": round(ref_bytes),
+                                       "gbs_if_read_from_hbm": round(ref_bytes / (kernel_ms * 1e-3) / 1e9, 1),
+                                       "note": "SURVEY §8(d) bytes of the reference's traversal; the kernel reads "
+                                               "its scene from caches, so this is not HBM traffic"}}
+    d = pmc_record(config, precision)
+    if d is None:
+        return r
+    valu = d["valu_insts_per_launch"] * share
+    ach = valu / (kernel_ms * 1e-3) / 1e9
+    r.update(achieved=round(ach, 1), frac=round(ach / VALU_PEAK_GINST, 4),
+             valu_insts_per_launch=round(valu), lane_utilisation=round(d["lane_utilisation"], 4),
+             pmc_round=d.get("round"), pmc_share_scale=round(share, 6))
+    if d.get("hbm_bytes_per_launch") is not None:
+        traffic = d["hbm_bytes_per_launch"] * share
+        r.update(traffic=round(traffic), hbm_gbs=round(traffic / (kernel_ms * 1e-3) / 1e9, 1),
+                 hbm_frac=round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+    return r
 
 
 def main():
@@ -119,6 +165,9 @@ def main():
     ap.add_argument("--row-block", type=int, default=1,
                     help="rows are dealt to ranks in blocks of this many (1: 600 rows split exactly 8 ways)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--precision", default="f64", choices=["f64", "f32"],
+                    help="the kernel precision of the line's value (f64: the reference's binary64)")
+    ap.add_argument("--no-f32", action="store_true", help="skip the FP32 fast-path record after an f64 line")
     ap.add_argument("--check", action="store_true", help="gather + assemble + sanity-check the frame after timing")
     ap.add_argument("--streams", type=int, default=0, choices=[0, 1, 2],
                     help="frames alternate between this many HIP streams (2: frame i+1 fills the CUs that "
@@ -163,127 +212,136 @@ def main():
     h, w, spp = image_height(cs), cs.cs_imageWidth, cs.cs_samplesPerPixel
     scene = DeviceScene(world, device=local_rank)
     rows = shard_rows(h, n_sh, args.row_block)
-    # two frame buffers: frame i+1 renders while the RCCL gather of frame i is in flight on the
-    # collective's own stream (the compute stream waits for gather i-1 before reusing its tile)
     if args.streams == 0:
         args.streams = 2 if scene.stats()["bvh_nodes"] == 0 else 1
-    nbuf = 2 if n > 1 or args.streams > 1 else 1
-    tiles = [torch.empty((rows, w, 3), dtype=torch.float32, device=dev) for _ in range(nbuf)]
-    gathered = [torch.empty((n * rows, w, 3), dtype=torch.float32, device=dev) for _ in range(nbuf)] if n > 1 else None
-    works = [None] * nbuf
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(args.streams - 1)]
 
-    ev = []
-    frame = [0]
+    def measure(precision):
+        """Warm up, then time exactly args.steps frames in `precision`; returns the rank's timings."""
+        dtype = torch.float64 if precision == "f64" else torch.float32
+        # two frame buffers: frame i+1 renders while the RCCL gather of frame i is in flight on the
+        # collective's own stream (the compute stream waits for gather i-1 before reusing its tile)
+        nbuf = 2 if n > 1 or args.streams > 1 else 1
+        tiles = [torch.empty((rows, w, 3), dtype=dtype, device=dev) for _ in range(nbuf)]
+        gathered = [torch.empty((n * rows, w, 3), dtype=dtype, device=dev) for _ in range(nbuf)] if n > 1 else None
+        works = [None] * nbuf
+        streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(args.streams - 1)]
+        ev = []
+        frame = [0]
 
-    def step(timed):
-        b = frame[0] % nbuf
-        stream = streams[frame[0] % len(streams)]
-        frame[0] += 1
-        with torch.cuda.stream(stream):
-            frame_step(b, stream, timed)
+        def step(timed):
+            b = frame[0] % nbuf
+            stream = streams[frame[0] % len(streams)]
+            frame[0] += 1
+            with torch.cuda.stream(stream):
+                frame_step(b, stream, timed)
 
-    def frame_step(b, stream, timed):
-        tile = tiles[b]
-        if works[b] is not None:
-            works[b].wait()  # stream-ordered: the gather that read this tile has completed
-            works[b] = None
-        if timed:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-        scene.render_async(cs, seed, tile.data_ptr(), stream.cuda_stream, n_shards=n_sh, shard=sh,
-                           row_block=args.row_block)
-        if timed:
-            e1.record(stream)
-            ev.append((e0, e1))
+        def frame_step(b, stream, timed):
+            tile = tiles[b]
+            if works[b] is not None:
+                works[b].wait()  # stream-ordered: the gather that read this tile has completed
+                works[b] = None
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            scene.render_async(cs, seed, tile.data_ptr(), stream.cuda_stream, n_shards=n_sh, shard=sh,
+                               row_block=args.row_block, precision=precision)
+            if timed:
+                e1.record(stream)
+                ev.append((e0, e1))
+            if n > 1:
+                if args.dist_backend == "nccl":
+                    works[b] = dist.all_gather_into_tensor(gathered[b], tile, async_op=True)
+                else:  # rehearsal path: through host memory
+                    parts = [torch.empty((rows, w, 3), dtype=dtype) for _ in range(n)]
+                    dist.all_gather(parts, tile.cpu())
+                    gathered[b].copy_(torch.cat(parts).to(dev))
+
+        def drain():
+            for k in range(nbuf):
+                if works[k] is not None:
+                    works[k].wait()
+                    works[k] = None
+            torch.cuda.synchronize(dev)
+
+        # untimed warm-up: W frames, and at least one per stream (a stream's first frame pays for its
+        # stream-ordered allocation pool); then, in rounds of doubling length, until the warm-up has
+        # kept the GPU busy for --warmup-s seconds: the per-frame time settles only after a few
+        # hundred ms of continuous rendering (Cornell 3.56 ms per frame after 2 warm-up frames, 3.47
+        # after 100; one rank's share of 8: 0.577 / 0.530 ms).  Ranks agree on every round (the
+        # gathers inside the frames must match), so they all run the same number of frames.
+        k, warm_frames, warm_s = max(args.warmup, len(streams)), 0, 0.0
+        while True:
+            tw = time.perf_counter()
+            for _ in range(k):
+                step(False)
+            drain()
+            warm_s += time.perf_counter() - tw
+            warm_frames += k
+            more = warm_s < args.warmup_s and warm_frames < 100000
+            if n > 1:
+                flag = torch.tensor([int(more)], dtype=torch.int32, device=dev if args.dist_backend == "nccl" else "cpu")
+                dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+                more = bool(flag.item())
+            if not more:
+                break
+            k = min(2 * k, 4096)
         if n > 1:
-            if args.dist_backend == "nccl":
-                works[b] = dist.all_gather_into_tensor(gathered[b], tile, async_op=True)
-            else:  # rehearsal path: through host memory
-                parts = [torch.empty((rows, w, 3), dtype=torch.float32) for _ in range(n)]
-                dist.all_gather(parts, tile.cpu())
-                gathered[b].copy_(torch.cat(parts).to(dev))
-
-    def drain():
-        for k in range(nbuf):
-            if works[k] is not None:
-                works[k].wait()
-                works[k] = None
+            dist.barrier()
         torch.cuda.synchronize(dev)
-
-    # untimed warm-up: W frames, and at least one per stream (a stream's first frame pays for its
-    # stream-ordered allocation pool); then, in rounds of doubling length, until the warm-up has
-    # kept the GPU busy for --warmup-s seconds: the per-frame time settles only after a few
-    # hundred ms of continuous rendering (Cornell 3.56 ms per frame after 2 warm-up frames, 3.47
-    # after 100; one rank's share of 8: 0.577 / 0.530 ms).  Ranks agree on every round (the
-    # gathers inside the frames must match), so they all run the same number of frames.
-    k, warm_frames, warm_s = max(args.warmup, len(streams)), 0, 0.0
-    while True:
-        tw = time.perf_counter()
-        for _ in range(k):
-            step(False)
-        drain()
-        warm_s += time.perf_counter() - tw
-        warm_frames += k
-        more = warm_s < args.warmup_s and warm_frames < 100000
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(True)
+        drain()  # every frame rendered AND gathered
         if n > 1:
-            flag = torch.tensor([int(more)], dtype=torch.int32, device=dev if args.dist_backend == "nccl" else "cpu")
-            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
-            more = bool(flag.item())
-        if not more:
-            break
-        k = min(2 * k, 4096)
-    if n > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-    drain()  # every frame rendered AND gathered
-    if n > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if n > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    # per-launch HIP-event duration, and the device time per frame: the HIP-event span of the timed
-    # frames / frames (with --streams 2 consecutive launches overlap, so a launch lasts longer than
-    # the device time it costs per frame)
-    launch_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
-    kernel_ms = launch_ms
-    if ev:
-        span = max(ev[0][0].elapsed_time(b) for _, b in ev[-len(streams):])
-        kernel_ms = span / len(ev)
-
-    check = None
-    if args.check or rank == 0:
-        import numpy as np
-        last = (frame[0] - 1) % nbuf
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
         if n > 1:
-            parts = gathered[last].view(n, rows, w, 3).cpu().numpy()
-            img = assemble_shards(parts, h, args.row_block)
-        else:
-            img = tiles[last][:h].cpu().numpy() if n_sh == 1 else tiles[last].cpu().numpy()
-        check = {"finite": bool(np.isfinite(img).all()), "mean_rgb": [round(float(x), 5) for x in img.reshape(-1, 3).mean(0)]}
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        # per-launch HIP-event duration, and the device time per frame: the HIP-event span of the
+        # timed frames / frames (with --streams 2 consecutive launches overlap, so a launch lasts
+        # longer than the device time it costs per frame)
+        launch_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
+        kernel_ms = launch_ms
+        if ev:
+            span = max(ev[0][0].elapsed_time(b) for _, b in ev[-len(streams):])
+            kernel_ms = span / len(ev)
+        check = None
+        if args.check or rank == 0:
+            import numpy as np
+            last = (frame[0] - 1) % nbuf
+            if n > 1:
+                parts = gathered[last].view(n, rows, w, 3).cpu().numpy()
+                img = assemble_shards(parts, h, args.row_block)
+            else:
+                img = tiles[last][:h].cpu().numpy() if n_sh == 1 else tiles[last].cpu().numpy()
+            check = {"finite": bool(np.isfinite(img).all()),
+                     "mean_rgb": [round(float(x), 5) for x in img.reshape(-1, 3).mean(0)]}
+        return dict(elapsed=elapsed, launch_ms=launch_ms, kernel_ms=kernel_ms, warm_frames=warm_frames,
+                    warm_s=warm_s, check=check, streams=len(streams))
+
+    precisions = [args.precision] + (["f32"] if args.precision == "f64" and not args.no_f32 else [])
+    res = {p: measure(p) for p in precisions}
 
     total_samples = h * w * spp
+    real_rows = int((shard_row_index(h, n_sh, sh, args.row_block) < h).sum())
     if n_sh != n:  # --sim-shards: the samples of the one shard rendered
-        total_samples = int((shard_row_index(h, n_sh, sh, args.row_block) < h).sum()) * w * spp
-    value = total_samples * args.steps / elapsed / 1e6
+        total_samples = real_rows * w * spp
+    samples_per_launch = real_rows * w * spp
+    share = samples_per_launch / (h * w * spp)  # of the full frame the PMC counts describe
     if rank == 0:
-        with open(os.path.join(ROOT, "tests", "golden", "algbytes.json")) as f:
-            alg = json.load(f)["configs"][args.config]
-        b_sample = alg["bytes_per_sample"]
-        real_rows = int((shard_row_index(h, n_sh, sh, args.row_block) < h).sum())
-        samples_per_launch = real_rows * w * spp
-        achieved = b_sample * samples_per_launch / (kernel_ms / 1e3) / 1e9
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.config),
-                    "kernel": "rt_render_kernel", "kernel_ms": round(kernel_ms, 4),
-                    "launch_ms": round(launch_ms, 4), "concurrent_launches": len(streams),
-                    "bytes_per_sample": round(b_sample, 1), "samples_per_launch": samples_per_launch}
+        def record(p):
+            r = res[p]
+            value = total_samples * args.steps / r["elapsed"] / 1e6
+            return value, {"value": round(value, 2), "unit": "Msamples/s", "dtype": p,
+                           "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 4),
+                           "warmup_frames": r["warm_frames"], "warmup_s": round(r["warm_s"], 3),
+                           "roofline": roofline_of(args.config, p, r["kernel_ms"], r["launch_ms"], share,
+                                                   samples_per_launch, r["streams"]),
+                           "check": r["check"]}
+        value, main_rec = record(precisions[0])
         cpu = None
         if n == 1 and not args.no_cpu_baseline:
             try:
@@ -293,19 +351,23 @@ def main():
         pub = PUBLISHED_MSAMPLES.get(args.config)
         line = {
             "metric": METRIC if args.config == "cornell" else f"Msamples/s, {args.config}",
-            "value": round(value, 2), "unit": "Msamples/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
-            "warmup_frames": warm_frames, "warmup_s": round(warm_s, 3),
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": round(value / pub, 1) if pub else None, "dtype": "f32",
+            "value": main_rec["value"], "unit": "Msamples/s", "n_gpus": n, "steps": args.steps,
+            "warmup": args.warmup, "warmup_frames": main_rec["warmup_frames"], "warmup_s": main_rec["warmup_s"],
+            "ms_per_step": main_rec["ms_per_step"], "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": round(value / pub, 1) if pub else None, "dtype": precisions[0],
             "data": "synthetic (reference scene built in-process, no external data)",
             "config": {"workload": f"{args.config} {w}x{h} {spp}spp depth {cs.cs_maxRecursionDepth}",
                        "width": w, "height": h, "spp": spp, "max_depth": cs.cs_maxRecursionDepth,
                        "parallelism": f"rows interleaved over {n} GPU(s), row_block {args.row_block}"
                                       + ((", RCCL all_gather of the framebuffer" if args.dist_backend == "nccl"
-                                          else ", gloo gather through host memory (rehearsal)") if n > 1 else "")},
-            "roofline": roofline, "issue_roofline": pmc_valu(args.config, kernel_ms), "cpu_baseline": cpu,
-            "check": check,
+                                          else ", gloo gather through host memory (rehearsal)") if n > 1 else "")
+                                      + (f" (diagnostic: shard 0 of {n_sh} only)" if n_sh != n else "")},
+            "roofline": main_rec["roofline"], "cpu_baseline": cpu, "check": main_rec["check"],
         }
+        if len(precisions) > 1:
+            _, f32 = record("f32")
+            f32["note"] = "FP32 fast path (rt_exec.flags RT_EXEC_F32), same frames, measured after the f64 line"
+            line["f32_fast_path"] = f32
         print(json.dumps(line), flush=True)
     if n > 1:
         dist.barrier()

@@ -16,19 +16,26 @@ from raytrace_amd import scenes  # noqa: E402
 
 
 def compare(name, cs, world, seed):
-    t0 = time.time()
-    st = {}
-    g = R.raytrace(cs, world, seed, stats=st)
-    t1 = time.time()
     o = oracle.render(cs, world, seed, mode=oracle.RNG_PHILOX)
-    t2 = time.time()
-    d = np.abs(g.astype(np.float64) - o)
-    rel = d / np.maximum(1.0, np.abs(o))
-    close = (rel.max(-1) < 1e-3).mean()
-    print(f"{name}: {g.shape} gpu {t1 - t0:.2f}s (kernel {st['kernel_ms']:.2f} ms) oracle {t2 - t1:.2f}s "
-          f"close(1e-3)={close:.4f} max={rel.max():.3g} mean gpu={g.reshape(-1, 3).mean(0)} "
-          f"oracle={o.reshape(-1, 3).mean(0)}", flush=True)
-    return close
+    out = {}
+    for prec in ("f64", "f32"):
+        t0 = time.time()
+        st = {}
+        g = R.raytrace(cs, world, seed, stats=st, precision=prec)
+        t1 = time.time()
+        d = np.abs(g.astype(np.float64) - o)
+        if prec == "f64":
+            rel = (d / np.maximum(np.abs(o), 1e-3)).max(-1)
+            close = float((rel <= 1e-9).mean())
+            tag = "<=1e-9 rel"
+        else:
+            rel = (d / np.maximum(1.0, np.abs(o))).max(-1)
+            close = float((rel < 1e-3).mean())
+            tag = "<1e-3"
+        print(f"{name} {prec}: {g.shape} gpu {t1 - t0:.2f}s (kernel {st['kernel_ms']:.2f} ms) close({tag})={close:.5f} "
+              f"max={rel.max():.3g} mean gpu={g.reshape(-1, 3).mean(0)} oracle={o.reshape(-1, 3).mean(0)}", flush=True)
+        out[prec] = close
+    return out
 
 
 if __name__ == "__main__":
@@ -38,12 +45,8 @@ if __name__ == "__main__":
     res["demo1"] = compare("demo1", *scenes.demo1(width=120, spp=8))
     res["bunny"] = compare("bunny", *scenes.bunny_cornell(width=64, spp=8))
     res["pawn_fog"] = compare("pawn_fog", *scenes.pawn_fog(width=64, spp=8))
-    # full-size Cornell timing
-    cs, world, seed = scenes.cornell_box()
-    st = {}
-    for _ in range(2):
-        img = R.raytrace(cs, world, seed, stats=st)
-    ms = st["kernel_ms"]
-    print(f"cornell 600x600x200: kernel {ms:.2f} ms -> {600 * 600 * 200 / ms / 1e3:.1f} Msamples/s, "
-          f"mean {img.reshape(-1, 3).mean(0)}", flush=True)
-    print("RESULT", res)
+    cs, world, seed = scenes.cornell_box(spp=4, width=50)
+    a = R.raytrace(cs, world, seed)
+    for devs in ([0, 0], [0, 0, 0]):
+        b = R.raytrace(cs, world, seed, devices=devs, row_block=1)
+        print(f"device list {devs}: bit-identical={np.array_equal(a, b)}", flush=True)
