@@ -8,7 +8,7 @@ for cfg in $CFGS; do
   for lib in base raytrace_amd/_lib/exp/*.so; do
     nm=$(basename $lib .so)
     if [ "$lib" = base ]; then unset RT_AMD_LIB; else export RT_AMD_LIB=$PWD/$lib; fi
-    timeout -k 10 200 python bench.py --no-cpu-baseline --config $n --steps $STEPS --sim-shards $sh > $OUT/${n}_${sh}_$nm.json 2>>$OUT/err.log || { echo "$nm failed"; exit 1; }
+    timeout -k 10 200 python bench.py --no-cpu-baseline --no-f32 --precision ${PREC:-f64} --config $n --steps $STEPS --sim-shards $sh > $OUT/${n}_${sh}_$nm.json 2>>$OUT/err.log || { echo "$nm failed"; exit 1; }
     python3 -c "import json;d=json.load(open('$OUT/${n}_${sh}_$nm.json'));print('$n shards $sh $nm', d['roofline']['kernel_ms'], d['ms_per_step'], d['check']['mean_rgb'])"
   done
 done
