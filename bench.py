@@ -131,7 +131,8 @@ def roofline_of(config, precision, kernel_ms, launch_ms, share, samples_per_laun
     frame, scaled by `share` = the fraction of the frame's samples this launch renders), measured
     HBM traffic beside it, and the reference-traversal bytes as a labelled figure."""
     with open(os.path.join(ROOT, "tests", "golden", "algbytes.json")) as f:
-        b_sample = json.load(f)["configs"][config]["bytes_per_sample"]
+        alg = json.load(f)["configs"]
+    b_sample = (alg.get(config) or alg[config.split("_")[0]])["bytes_per_sample"]  # demo1_1200x800: demo1's
     ref_bytes = b_sample * samples_per_launch
     r = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_GINST, "unit": "G VALU wave-instr/s", "frac": None,
          "traffic": None, "kernel": "rt_render_kernel", "precision": precision, "kernel_ms": round(kernel_ms, 4),
@@ -161,7 +162,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="cornell", choices=["cornell", "readme", "demo1", "bunny_cornell", "pawn_fog"])
+    ap.add_argument("--config", default="cornell", choices=["cornell", "readme", "demo1", "demo1_1200x800", "bunny_cornell", "pawn_fog"])
     ap.add_argument("--row-block", type=int, default=1,
                     help="rows are dealt to ranks in blocks of this many (1: 600 rows split exactly 8 ways)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -15,6 +15,7 @@
 
 #include "../../include/rt.h"
 #include "rt_bvh.h"
+#include "rt_encode8_table.h"
 #include "rt_internal.h"
 
 namespace {
@@ -892,36 +893,9 @@ template int rt_host_make_params<double>(const rt_camera_settings*, uint64_t, co
 template void rt_host_plan_work<float>(KernelParamsT<float>&, long long);
 template void rt_host_plan_work<double>(KernelParamsT<double>&, long long);
 
-// The 8-bit code of writeImage / writeImageSqrt's quantisation, exactly as the host encoder
-// computes it (raytrace_amd.ray.encode8: binary64, libm pow / sqrt).
-static int encode8_code(double x, int encoding) {
-  x = std::isnan(x) ? 0.0 : std::min(1.0, std::max(0.0, x));
-  const double t = encoding == 1 ? std::sqrt(x) : (x <= 0.0031308 ? 12.92 * x : 1.055 * std::pow(x, 1 / 2.4) - 0.055);
-  const double c = std::floor(256.0 * t);
-  return c > 255.0 ? 255 : (int)c;
-}
-
+// The 8-bit code thresholds of writeImage / writeImageSqrt's quantisation (rt_encode8_table.h,
+// generated with the transfer evaluated exactly; raytrace_amd.ray.encode8 reads the same table).
 void rt_host_encode8_thresholds(int encoding, double* thr) {
-  // the code is monotone in x; binary search over the ordered bit patterns of [0, 1]
-  thr[0] = 0.0;
-  for (int k = 1; k < 256; ++k) {
-    uint64_t lo = 0, hi = 0x3FF0000000000000ull;  // code(lo) < k <= code(hi) (code(1) = 255)
-    auto at = [](uint64_t b) {
-      double d;
-      std::memcpy(&d, &b, 8);
-      return d;
-    };
-    if (encode8_code(0.0, encoding) >= k) {
-      thr[k] = 0.0;
-      continue;
-    }
-    while (hi - lo > 1) {
-      const uint64_t mid = lo + (hi - lo) / 2;
-      if (encode8_code(at(mid), encoding) >= k)
-        hi = mid;
-      else
-        lo = mid;
-    }
-    thr[k] = at(hi);
-  }
+  const double* t = encoding == 1 ? kEnc8Sqrt : kEnc8Srgb;
+  for (int k = 0; k < 256; ++k) thr[k] = t[k];
 }

@@ -17,18 +17,17 @@
 #include "rt_render_kernel.h"
 
 // Output epilogue of writeImage / writeImageSqrt (Ray.hs:248-260): 8-bit codes
-// min(255, floor(256 * transfer(clamp01 x))), transfer = sRGB or sqrt, BIT-EXACT against the host
-// encoder (raytrace_amd.ray.encode8, binary64 libm): the host tabulates, per code k, the smallest
-// binary64 x whose code is >= k (rt_build.cpp rt_host_encode8_thresholds, the same libm), and the
-// device takes its first guess from the binary64 transfer and corrects it against that monotone
-// table (the guess is off by at most one code where 256 transfer(x) rounds across an integer).
-// NaN encodes as 0.  Memory-bound: 4 values per lane, 16 B (float) / 32 B (binary64) in, 4 B out.
+// min(255, floor(256 * transfer(clamp01 x))), transfer = sRGB or sqrt, as the number of code
+// thresholds <= x (rt_encode8_table.h: per code, the smallest binary64 with that code under the
+// exactly evaluated transfer) — a binary search in an LDS copy of the 256-entry table, no
+// transcendental, so the device codes equal the host encoder's (raytrace_amd.ray.encode8, same
+// table) bit for bit on every input.  NaN encodes as 0.  Memory-bound: 4 values per lane.
 struct Enc8Table {
   double thr[256];
 };
 template <bool kF64>
 __global__ __launch_bounds__(256) void rt_encode8_kernel(const void* __restrict__ in_, uint8_t* __restrict__ out,
-                                                         int64_t n, Enc8Table T, int encoding) {
+                                                         int64_t n, Enc8Table T) {
   __shared__ double thr[256];
   thr[threadIdx.x] = T.thr[threadIdx.x];
   __syncthreads();
@@ -36,18 +35,13 @@ __global__ __launch_bounds__(256) void rt_encode8_kernel(const void* __restrict_
   const double* ind = (const double*)in_;
   int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   for (; i < n; i += (int64_t)gridDim.x * 256 * 4) {
-    double v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = (i + k < n) ? (kF64 ? ind[i + k] : (double)inf[i + k]) : 0.0;
     uint32_t packed = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const double x = v[k] != v[k] ? 0.0 : fmin(1.0, fmax(0.0, v[k]));
-      const double e = encoding == 1 ? sqrt(x) : (x <= 0.0031308 ? 12.92 * x : 1.055 * pow(x, 1.0 / 2.4) - 0.055);
-      int code = (int)floor(256.0 * e);
-      code = code > 255 ? 255 : (code < 0 ? 0 : code);
-      if (code < 255 && x >= thr[code + 1]) ++code;
-      if (code > 0 && x < thr[code]) --code;
+      const double x = (i + k < n) ? (kF64 ? ind[i + k] : (double)inf[i + k]) : 0.0;
+      int code = 0;  // largest k with thr[k] <= x (thr[0] = 0; NaN and x < thr[1] -> 0)
+#pragma unroll
+      for (int step = 128; step >= 1; step >>= 1) code = thr[code + step] <= x ? code + step : code;
       packed |= (uint32_t)code << (8 * k);
     }
     if (i + 4 <= n && ((reinterpret_cast<uintptr_t>(out + i) & 3) == 0)) {
@@ -60,6 +54,7 @@ __global__ __launch_bounds__(256) void rt_encode8_kernel(const void* __restrict_
 
 int rt_launch_encode8(const void* in, int in_f64, uint8_t* out, int64_t n, const double* thr, int encoding,
                       void* stream) {
+  (void)encoding;  // the table is the encoding
   if (n <= 0) return 0;
   int64_t blocks = (n / 4 + 255) / 256 + 1;
   if (blocks > 4096) blocks = 4096;
@@ -67,9 +62,9 @@ int rt_launch_encode8(const void* in, int in_f64, uint8_t* out, int64_t n, const
   for (int k = 0; k < 256; ++k) T.thr[k] = thr[k];
   if (in_f64)
     hipLaunchKernelGGL(rt_encode8_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, in, out, n,
-                       T, encoding);
+                       T);
   else
     hipLaunchKernelGGL(rt_encode8_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, in, out, n,
-                       T, encoding);
+                       T);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -143,17 +143,31 @@ class DeviceScene:
 
 # ------------------------------------------------------------------ image IO (Ray.hs:240-260)
 
+_ENC8 = None
+
+
+def encode8_thresholds(encoding: str = "srgb") -> np.ndarray:
+    """Per 8-bit code k, the smallest binary64 x whose code is >= k under the EXACTLY evaluated
+    transfer (raytrace_amd/data/encode8_thresholds.json, tools/gen_encode8_table.py); the device
+    epilogue reads the same table (rt_encode8_table.h)."""
+    global _ENC8
+    if _ENC8 is None:
+        import json
+        import os
+        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "encode8_thresholds.json")) as f:
+            d = json.load(f)
+        _ENC8 = {k: np.array([float.fromhex(x) for x in d[k]]) for k in ("srgb", "sqrt")}
+    return _ENC8["sqrt" if encoding == "sqrt" else "srgb"]
+
+
 def encode8(rgb: np.ndarray, encoding: str = "srgb") -> np.ndarray:
     """8-bit codes as the reference's writers store them: min(255, floor(256 * transfer(clamp01 x)))
-    with transfer = sRGB (writeImage) or sqrt (writeImageSqrt); NaN -> 0.  Host twin of
-    rt_encode8_async (which is bit-exact against it)."""
+    with transfer = sRGB (writeImage) or sqrt (writeImageSqrt), the transfer evaluated exactly (the
+    number of code thresholds <= x); NaN -> 0.  Host twin of rt_encode8_async (bit-exact with it)."""
     x = np.asarray(rgb, np.float64)
-    x = np.clip(np.where(np.isnan(x), 0.0, x), 0.0, 1.0)
-    if encoding == "sqrt":
-        t = np.sqrt(x)
-    else:
-        t = np.where(x <= 0.0031308, 12.92 * x, 1.055 * np.power(x, 1 / 2.4) - 0.055)
-    return np.minimum(np.floor(256.0 * t), 255).astype(np.uint8)
+    thr = encode8_thresholds(encoding)
+    codes = np.searchsorted(thr[1:], np.where(np.isnan(x), -1.0, x), side="right")
+    return codes.astype(np.uint8)
 
 
 def _write_png(path: str, codes: np.ndarray):

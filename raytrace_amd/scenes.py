@@ -115,13 +115,21 @@ def demo1_world(gen):
     return bvhTree(big + small), gen
 
 
-def demo1(width=1200, spp=500, depth=50, seed=1):
+def demo1(width=1200, spp=500, depth=50, seed=1, aspect=16 / 9):
+    """test/Main.hs:136-186 (aspect 16/9: 1200 x 675, the reference's own image size)."""
     world, gen2 = demo1_world(mkStdGen(seed))
     settings = defaultCameraSettings(
-        cs_aspectRatio=16 / 9, cs_imageWidth=width, cs_samplesPerPixel=spp, cs_maxRecursionDepth=depth,
+        cs_aspectRatio=aspect, cs_imageWidth=width, cs_samplesPerPixel=spp, cs_maxRecursionDepth=depth,
         cs_vfov=degrees(20), cs_center=V3(13, 2, 3), cs_lookAt=V3(0, 0, 0), cs_defocusAngle=degrees(0.6),
         cs_focusDist=10, cs_background=sky)
     return settings, world, gen2
+
+
+def demo1_1200x800(width=1200, spp=500, depth=50, seed=1):
+    """demo1 at BASELINE.json's 1200 x 800 (aspect 3/2).  The reference renders 1200 x 675
+    (test/Main.hs:170-172, aspect 16/9); BASELINE.json's configs line says 1200x800, so both
+    are provided."""
+    return demo1(width=width, spp=spp, depth=depth, seed=seed, aspect=3 / 2)
 
 
 def load_mesh(name):
@@ -205,6 +213,7 @@ CONFIGS = {
     "readme": readme_scene,
     "cornell": cornell_box,
     "demo1": demo1,
+    "demo1_1200x800": demo1_1200x800,
     "bunny_cornell": bunny_cornell,
     "pawn_fog": pawn_fog,
     "pawn_test": pawn_test,

@@ -1,15 +1,24 @@
-"""GPU parity tests (MI355X): the HIP kernel through the C ABI against the FP64 oracle.
+"""GPU parity tests (MI355X): the HIP kernels through the C ABI against the FP64 oracle.
 
-Tolerances:
-  * per pixel, same Philox numbers (oracle Philox mode): every channel within 1e-3 (relative
-    above 1) for >= 99 % of pixels (>= 97 % on demo1's glass/metal spheres); FP32 vs FP64 paths
-    only split where a decision sits within rounding of its threshold;
-  * image means within 0.5 % of the oracle's at the same seed;
+The oracle's Philox mode consumes the same random numbers as the device, so images compare
+per pixel.  Tolerances (reference precision is binary64, Core.hs:29-31):
+  * binary64 kernel (the default): >= 99.9 % of pixels within 1e-9 relative of the oracle
+    (max(|ref|, 1e-3) scale) — the remaining pixels hold a sample whose path split on a
+    decision within rounding of its threshold; the worst pixel within 2 L / spp of the oracle,
+    L = the largest radiance one sample can carry in the scene (the brightest emitter or
+    background; a divergent sample moves its pixel's mean by at most L / spp), i.e. at most
+    two divergent samples in any pixel;
+  * FP32 kernel (RT_EXEC_F32): >= 99 % of pixels within 1e-3 (relative above 1; >= 97 % on
+    demo1's glass / metal spheres), the worst pixel within 4 L / spp + 1e-3;
+  * both: per-channel 8x8-block RMSE against the oracle <= 0.5 x the seed-to-seed noise floor
+    of the published renders (FP32 on the glass-cuboid test scene: 1.5 x), means within 0.5 %;
   * full-size Cornell box vs the reference's cornell_box_redirect.png: 8x8-block RMSE within
-    1.5x the measured seed-to-seed noise floor, means within 1 % (SURVEY.md §8c);
-  * row-sharded renders reassemble bit-identically; repeated renders are bit-identical.
+    1.5x the measured seed-to-seed noise floor, means within 1 %;
+  * row-sharded renders, device lists and item chunkings are bit-identical; repeated renders
+    are bit-identical; the 8-bit epilogue equals the host encoder bit for bit.
 """
 import ctypes
+import json
 import os
 
 import numpy as np
@@ -22,14 +31,45 @@ pytestmark = pytest.mark.gpu
 import raytrace_amd as R  # noqa: E402
 from raytrace_amd import scenes  # noqa: E402
 
+# (name, scene, kwargs, FP32 per-pixel bar, L = the largest radiance of one sample: the Cornell
+# light (15) or the background / sky (1))
 CASES = [
-    ("cornell", scenes.cornell_box, dict(spp=16, width=96), 0.99),
-    ("readme", scenes.readme_scene, dict(spp=16, width=120), 0.99),
-    ("demo1", scenes.demo1, dict(width=160, spp=8), 0.97),
-    ("bunny_cornell", scenes.bunny_cornell, dict(width=80, spp=8), 0.99),
-    ("pawn_fog", scenes.pawn_fog, dict(width=80, spp=8), 0.99),
-    ("pawn_test", scenes.pawn_test, dict(width=80, spp=8), 0.99),
+    ("cornell", scenes.cornell_box, dict(spp=16, width=96), 0.99, 15.0),
+    ("readme", scenes.readme_scene, dict(spp=16, width=120), 0.99, 1.0),
+    ("demo1", scenes.demo1, dict(width=160, spp=8), 0.97, 1.0),
+    ("bunny_cornell", scenes.bunny_cornell, dict(width=80, spp=8), 0.99, 15.0),
+    ("pawn_fog", scenes.pawn_fog, dict(width=80, spp=8), 0.99, 1.0),
+    ("pawn_test", scenes.pawn_test, dict(width=80, spp=8), 0.99, 1.0),
 ]
+
+
+def _floor():
+    with open(os.path.join(GOLDEN, "noise_floor.json")) as f:
+        d = json.load(f)
+    return {"cornell": np.array(d["cornell_box_redirect"]["block8_rmse"]),
+            "readme": np.array(d["example_image"]["block8_rmse"])}
+
+
+def assert_parity(img, ref, precision, need32=0.99, floor=None, what="", spp=8, lmax=1.0, floor_mult=0.5):
+    """The file docstring's per-pixel, worst-pixel, block and mean bars."""
+    assert img.shape == ref.shape
+    assert img.dtype == (np.float64 if precision == "f64" else np.float32)
+    assert np.isfinite(img).all(), what
+    d = np.abs(img.astype(np.float64) - ref)
+    if precision == "f64":
+        rel = (d / np.maximum(np.abs(ref), 1e-3)).max(-1)
+        frac = float((rel <= 1e-9).mean())
+        assert frac >= 0.999, (what, frac)
+        assert d.max() <= 2 * lmax / spp, (what, float(d.max()), 2 * lmax / spp)
+    else:
+        rel = (d / np.maximum(np.abs(ref), 1.0)).max(-1)
+        frac = float((rel < 1e-3).mean())
+        assert frac >= need32, (what, frac)
+        assert d.max() <= 4 * lmax / spp + 1e-3, (what, float(d.max()), 4 * lmax / spp)
+    if floor is not None and img.shape[0] >= 8 and img.shape[1] >= 8:
+        rmse = np.sqrt(((block8(img.astype(np.float64)) - block8(ref)) ** 2).reshape(-1, 3).mean(0))
+        assert (rmse <= floor_mult * floor).all(), (what, rmse, floor_mult * floor)
+    np.testing.assert_allclose(img.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=5e-3, atol=1e-6)
 
 
 @pytest.fixture(scope="module")
@@ -41,30 +81,62 @@ def gpu():
     return torch
 
 
-@pytest.mark.parametrize("name,fn,kw,need", CASES, ids=[c[0] for c in CASES])
-def test_gpu_matches_oracle_per_pixel(gpu, oracle_mod, name, fn, kw, need):
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("name,fn,kw,need,lmax", CASES, ids=[c[0] for c in CASES])
+def test_gpu_matches_oracle_per_pixel(gpu, oracle_mod, name, fn, kw, need, lmax, precision):
     cs, world, seed = fn(**kw)
-    img = R.raytrace(cs, world, seed)
+    img = R.raytrace(cs, world, seed, precision=precision)
     ref = oracle_mod.render(cs, world, seed, mode=oracle_mod.RNG_PHILOX)
-    assert img.shape == ref.shape and img.dtype == np.float32
-    assert np.isfinite(img).all()
-    assert pixel_agreement(img, ref) >= need
-    np.testing.assert_allclose(img.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=5e-3)
+    assert_parity(img, ref, precision, need, _floor()["cornell"], name, kw["spp"], lmax)
 
 
-def test_gpu_matches_kernel_emulator(gpu, emu_mod):
-    """Same source (rt_trace.h) on the host: identical numbers up to FP contraction / libm."""
+# Every BASELINE config at its FULL resolution (reduced spp), compared with the oracle on every
+# 8th row: the per-pixel, worst-pixel, 8x8-block (over the sampled rows) and mean bars.
+FULL = [
+    ("readme", scenes.readme_scene, dict(spp=8), "readme", 1.0),
+    ("cornell", scenes.cornell_box, dict(spp=8), "cornell", 15.0),
+    ("demo1", scenes.demo1, dict(spp=4), "cornell", 1.0),
+    ("demo1_1200x800", scenes.demo1_1200x800, dict(spp=2), "cornell", 1.0),
+    ("bunny_cornell", scenes.bunny_cornell, dict(spp=4), "cornell", 15.0),
+    ("pawn_fog", scenes.pawn_fog, dict(spp=4), "cornell", 1.0),
+]
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("name,fn,kw,fl,lmax", FULL, ids=[c[0] for c in FULL])
+def test_full_resolution_parity_on_row_subset(gpu, oracle_mod, name, fn, kw, fl, lmax, precision):
+    from raytrace_amd.camera import image_height
+    cs, world, seed = fn(**kw)
+    h, w = image_height(cs), int(cs.cs_imageWidth)
+    img = R.raytrace(cs, world, seed, precision=precision)
+    assert img.shape == (h, w, 3)
+    rows = np.arange(0, h, 8)
+    pix = (rows[:, None] * w + np.arange(w)[None, :]).reshape(-1).astype(np.int32)
+    ref = oracle_mod.render(cs, world, seed, mode=oracle_mod.RNG_PHILOX, pixels=pix).reshape(len(rows), w, 3)
+    need = 0.97 if name.startswith("demo1") else 0.99
+    assert_parity(img[rows], ref, precision, need, _floor()[fl], name, kw["spp"], lmax)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_gpu_matches_kernel_emulator(gpu, emu_mod, precision):
+    """Same source (rt_trace.h) on the host: identical numbers up to FP contraction / libm (the
+    device's Newton-refined binary64 reciprocals and its sin / cos polynomial differ from the
+    host's IEEE / libm results by ulps)."""
     cs, world, seed = scenes.cornell_box(spp=8, width=64)
-    a = R.raytrace(cs, world, seed)
-    b = emu_mod.render(cs, world, seed)
-    assert pixel_agreement(a, b, 1e-4) > 0.99
+    a = R.raytrace(cs, world, seed, precision=precision)
+    b = emu_mod.render(cs, world, seed, precision=precision)
+    if precision == "f64":
+        rel = (np.abs(a - b) / np.maximum(np.abs(b), 1e-3)).max(-1)
+        assert (rel <= 1e-9).mean() >= 0.999
+    else:
+        assert pixel_agreement(a, b, 1e-4) > 0.99
 
 
 def test_full_cornell_matches_published_render(gpu, golden_stats):
     stats, floors = golden_stats
     cs, world, seed = scenes.cornell_box()
     img = R.raytrace(cs, world, seed)
-    assert img.shape == (600, 600, 3)
+    assert img.shape == (600, 600, 3) and img.dtype == np.float64
     lin = as_published(img, "sqrt")
     gold = np.load(os.path.join(GOLDEN, "cornell_box_redirect_block8.npy")).astype(np.float64)
     rmse = np.sqrt(((block8(lin) - gold) ** 2).reshape(-1, 3).mean(0))
@@ -93,19 +165,21 @@ def test_pawn_demo_matches_published_render(gpu, golden_stats):
     assert np.sqrt(((block8(lin) - gold) ** 2).mean()) < 0.02
 
 
-def test_full_demo1_is_finite(gpu):
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_full_demo1_is_finite(gpu, precision):
     """demo1 at its full 1200x675x500: long total-internal-reflection chains inside the glass
     spheres stay finite (directions re-normalised after reflect / refract, rt_trace.h `unit`)."""
     cs, world, seed = scenes.demo1()
-    img = R.raytrace(cs, world, seed)
+    img = R.raytrace(cs, world, seed, precision=precision)
     assert img.shape == (675, 1200, 3)
     assert np.isfinite(img).all()
     m = img.reshape(-1, 3).mean(0)
     assert (m > 0.3).all() and (m < 1.0).all()
 
 
+@pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("name", ["cornell", "pawn_fog", "bunny_cornell", "demo1"])
-def test_kernel_variants_bitwise_identical(gpu, monkeypatch, name):
+def test_kernel_variants_bitwise_identical(gpu, monkeypatch, name, precision):
     """Flat / BVH-lockstep / BVH-decoupled kernels: same per-path arithmetic, different schedule;
     fixed-point accumulation makes the images bit-identical."""
     fn = {"cornell": scenes.cornell_box, "pawn_fog": scenes.pawn_fog, "bunny_cornell": scenes.bunny_cornell,
@@ -117,37 +191,43 @@ def test_kernel_variants_bitwise_identical(gpu, monkeypatch, name):
     monkeypatch.setenv("RT_AMD_NO_BOX", "1")
     for v in ("0", "1", "2"):
         monkeypatch.setenv("RT_AMD_VARIANT", v)
-        imgs.append(R.raytrace(cs, world, seed))
+        imgs.append(R.raytrace(cs, world, seed, precision=precision))
     for img in imgs[1:]:
         assert np.array_equal(img, imgs[0], equal_nan=True)
 
 
+@pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("name", ["bunny_cornell", "demo1"])
-def test_large_primitive_prefix_is_exact(gpu, monkeypatch, name):
+def test_large_primitive_prefix_is_exact(gpu, monkeypatch, name, precision):
     fn = {"bunny_cornell": scenes.bunny_cornell, "demo1": scenes.demo1}[name]
     cs, world, seed = fn(width=96, spp=8)
     monkeypatch.setenv("RT_AMD_NO_BOX", "1")  # exact claim: per-face tests in and out of the BVH
-    a = R.raytrace(cs, world, seed)
+    a = R.raytrace(cs, world, seed, precision=precision)
     monkeypatch.setenv("RT_AMD_NO_PREFIX", "1")
-    b = R.raytrace(cs, world, seed)
+    b = R.raytrace(cs, world, seed, precision=precision)
     assert np.array_equal(a, b, equal_nan=True)
 
 
+@pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("name", ["cornell", "box_gallery"])
-def test_box_groups_match_oracle(gpu, oracle_mod, monkeypatch, name):
+def test_box_groups_match_oracle(gpu, oracle_mod, monkeypatch, name, precision):
     fn = {"cornell": scenes.cornell_box, "box_gallery": scenes.box_gallery}[name]
     cs, world, seed = fn(width=96, spp=8)
-    a = R.raytrace(cs, world, seed)
+    a = R.raytrace(cs, world, seed, precision=precision)
     ref = oracle_mod.render(cs, world, seed, mode=oracle_mod.RNG_PHILOX)
-    assert np.isfinite(a).all()
-    assert pixel_agreement(a, ref) >= 0.99
+    # FP32 on box_gallery's oblique glass cuboid at 8 spp: paths that split on a rounding-level
+    # decision inside the glass carry the light's 15 to a different pixel, so the block bar is
+    # the 1.5x of §8c's CPU-vs-reference test there; binary64 keeps 0.5x
+    mult = 1.5 if (precision == "f32" and name == "box_gallery") else 0.5
+    assert_parity(a, ref, precision, 0.99, _floor()["cornell"], name, 8, 15.0, mult)
     monkeypatch.setenv("RT_AMD_NO_BOX", "1")
-    b = R.raytrace(cs, world, seed)
-    assert pixel_agreement(a, b) >= 0.995
+    b = R.raytrace(cs, world, seed, precision=precision)
+    assert pixel_agreement(a, b, 1e-9 if precision == "f64" else 1e-3) >= 0.995
 
 
+@pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("name", ["cornell", "bunny_cornell"])
-def test_item_chunk_does_not_change_the_image(gpu, monkeypatch, name):
+def test_item_chunk_does_not_change_the_image(gpu, monkeypatch, name, precision):
     """Items of 1, 3 (ragged: does not divide spp), 4 and 16 samples: a different work split
     and commit order, the same fixed-point sums — bit-identical images."""
     fn = {"cornell": scenes.cornell_box, "bunny_cornell": scenes.bunny_cornell}[name]
@@ -155,16 +235,17 @@ def test_item_chunk_does_not_change_the_image(gpu, monkeypatch, name):
     imgs = []
     for c in ("1", "3", "4", "16"):
         monkeypatch.setenv("RT_AMD_CHUNK", c)
-        imgs.append(R.raytrace(cs, world, seed))
+        imgs.append(R.raytrace(cs, world, seed, precision=precision))
     for img in imgs[1:]:
         assert np.array_equal(img, imgs[0], equal_nan=True)
 
 
-def test_medium_boundary_alias_is_exact(gpu, monkeypatch):
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_medium_boundary_alias_is_exact(gpu, monkeypatch, precision):
     cs, world, seed = scenes.pawn_fog(width=96, spp=8)
-    a = R.raytrace(cs, world, seed)
+    a = R.raytrace(cs, world, seed, precision=precision)
     monkeypatch.setenv("RT_AMD_NO_ALIAS", "1")
-    b = R.raytrace(cs, world, seed)
+    b = R.raytrace(cs, world, seed, precision=precision)
     assert np.array_equal(a, b, equal_nan=True)
 
 
@@ -177,40 +258,54 @@ def _image_scene():
     return R.defaultCameraSettings(cs_imageWidth=120, cs_samplesPerPixel=8, cs_background=R.sky), world, R.mkStdGen(3)
 
 
+@pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("name", ["noise_test", "image"])
-def test_textured_scenes_match_oracle_per_pixel(gpu, oracle_mod, name):
+def test_textured_scenes_match_oracle_per_pixel(gpu, oracle_mod, name, precision):
     """imageTexture (wrap, row flip) and the Perlin noise / marble textures (Texture.hs:31-78,
     Noise.hs) against the oracle on the same Philox numbers."""
     cs, world, seed = scenes.noise_test(width=160, spp=8) if name == "noise_test" else _image_scene()
-    img = R.raytrace(cs, world, seed)
+    img = R.raytrace(cs, world, seed, precision=precision)
     ref = oracle_mod.render(cs, world, seed, mode=oracle_mod.RNG_PHILOX)
-    assert np.isfinite(img).all()
-    assert pixel_agreement(img, ref) >= 0.99
-    np.testing.assert_allclose(img.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=5e-3)
+    assert_parity(img, ref, precision, 0.99, _floor()["cornell"], name, 8, 1.0)
 
 
+@pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("kind", ["sphere", "triangle", "parallelogram", "mirror"])
-def test_known_answer_hits(gpu, kind):
+def test_known_answer_hits(gpu, kind, precision):
     """The analytic known-answer scenes of test_oracle_golden on the GPU:
     pixels wholly inside / outside the primitive are exact."""
     from test_oracle_golden import _kat_scene
     cs, world, mask = _kat_scene(kind)
-    out = R.raytrace(cs, world, R.mkStdGen(5))
+    out = R.raytrace(cs, world, R.mkStdGen(5), precision=precision)
     m = mask >= 0
-    np.testing.assert_allclose(out[m], np.repeat(mask[m][:, None], 3, axis=1), atol=1e-6)
+    np.testing.assert_allclose(out[m], np.repeat(mask[m][:, None], 3, axis=1), atol=1e-12 if precision == "f64" else 1e-6)
 
 
-def test_deterministic_and_shard_invariant(gpu):
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_deterministic_shard_and_device_list_invariant(gpu, precision):
+    """Repeated renders, row shards (one process per GPU) and device lists (one process, many
+    GPUs: ABI v3 rt_exec.devices, here device 0 listed 2 and 3 times) all give the same image."""
     from raytrace_amd.ray import assemble_shards, render_shard
     cs, world, seed = scenes.cornell_box(spp=4, width=50)
-    a = R.raytrace(cs, world, seed)
-    b = R.raytrace(cs, world, seed)
+    a = R.raytrace(cs, world, seed, precision=precision)
+    b = R.raytrace(cs, world, seed, precision=precision)
     np.testing.assert_array_equal(a, b)
     for n, rb in [(2, 4), (3, 1), (8, 4)]:
-        tiles = np.stack([render_shard(cs, world, seed, n, r, rb) for r in range(n)])
+        tiles = np.stack([render_shard(cs, world, seed, n, r, rb, precision=precision) for r in range(n)])
         np.testing.assert_array_equal(assemble_shards(tiles, 50, rb), a)
-    c = R.raytrace(cs, world, R.mkStdGen(235))
-    assert not np.array_equal(a, c)
+    for devs, rb in [([0, 0], 4), ([0, 0, 0], 1), ([0] * 8, 2)]:
+        st = {}
+        c = R.raytrace(cs, world, seed, precision=precision, devices=devs, row_block=rb, stats=st)
+        np.testing.assert_array_equal(c, a)
+        assert st["samples"] == 50 * 50 * 4
+    d = R.raytrace(cs, world, R.mkStdGen(235), precision=precision)
+    assert not np.array_equal(a, d)
+
+
+def test_device_list_bvh_scene(gpu):
+    cs, world, seed = scenes.bunny_cornell(width=64, spp=4)
+    a = R.raytrace(cs, world, seed)
+    np.testing.assert_array_equal(R.raytrace(cs, world, seed, devices=[0, 0, 0], row_block=1), a)
 
 
 def test_edge_cases(gpu):
@@ -225,15 +320,17 @@ def test_edge_cases(gpu):
     # a world that is a single sphere (root of the BVH is a leaf) under a sky background
     sky_world = R.lambertian(R.constantTexture(0.5)) << R.sphere((0, 0, -1), 0.5)
     img = R.raytrace(R.defaultCameraSettings(cs_imageWidth=32, cs_background=R.sky), sky_world, R.mkStdGen(1))
-    assert np.isfinite(img).all() and img.max() <= 1.0 + 1e-6
-    # background only: every sample sees const colour exactly
+    assert np.isfinite(img).all() and img.max() <= 1.0 + 1e-12
+    # background only: every sample sees const colour exactly, in both precisions
     empty_like = R.lightSource(R.constantTexture(0)) << R.sphere((0, 0, 100), 0.1)
-    bg = R.raytrace(R.defaultCameraSettings(cs_imageWidth=8, cs_background=R.constBackground((0.25, 0.5, 1.0))),
-                    empty_like, R.mkStdGen(3))
-    np.testing.assert_array_equal(bg, np.broadcast_to(np.float32([0.25, 0.5, 1.0]), bg.shape))
+    for precision in ("f64", "f32"):
+        bg = R.raytrace(R.defaultCameraSettings(cs_imageWidth=8, cs_background=R.constBackground((0.25, 0.5, 1.0))),
+                        empty_like, R.mkStdGen(3), precision=precision)
+        np.testing.assert_array_equal(bg, np.broadcast_to(np.array([0.25, 0.5, 1.0]), bg.shape))
 
 
-def test_all_materials_against_oracle(gpu, oracle_mod):
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_all_materials_against_oracle(gpu, oracle_mod, precision):
     """One sphere per reference material (Material.hs:41-129) over a checker floor, media included."""
     mats = [R.lightSource(R.constantTexture(4)), R.pitchBlack, R.lambertian(R.constantTexture((0.7, 0.3, 0.2))),
             R.lommelSeeliger(R.constantTexture(0.9)), R.mirror(R.constantTexture(0.8)),
@@ -251,13 +348,13 @@ def test_all_materials_against_oracle(gpu, oracle_mod):
     cs = R.defaultCameraSettings(cs_imageWidth=160, cs_aspectRatio=2.0, cs_samplesPerPixel=8, cs_background=R.sky,
                                  cs_center=(0, 1, 2), cs_lookAt=(0, -0.5, -4),
                                  cs_redirectTargets=[(0.2, (-5, 3, -5), (10, 0, 0), (0, 0, 2))])
-    img = R.raytrace(cs, world, R.mkStdGen(9))
+    img = R.raytrace(cs, world, R.mkStdGen(9), precision=precision)
     ref = oracle_mod.render(cs, world, R.mkStdGen(9), mode=oracle_mod.RNG_PHILOX)
-    assert pixel_agreement(img, ref) >= 0.98
-    np.testing.assert_allclose(img.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=5e-3)
+    assert_parity(img, ref, precision, 0.98, _floor()["cornell"], "materials", 8, 4.0)
 
 
-def test_moving_and_transform_against_oracle(gpu, oracle_mod):
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_moving_and_transform_against_oracle(gpu, oracle_mod, precision):
     """`moving` (motion blur, Geometry.hs:449-456) and rotated textured spheres (sphereUV frame)."""
     tex = R.checkerTexture(8, 4, (0.9, 0.1, 0.1), (0.1, 0.1, 0.9))
     world = R.group([
@@ -270,29 +367,49 @@ def test_moving_and_transform_against_oracle(gpu, oracle_mod):
                                                                      R.cuboid(R.fromCorners((-2, -0.5, -3.5), (-1.2, 0.5, -2.7))))),
     ])
     cs = R.defaultCameraSettings(cs_imageWidth=128, cs_aspectRatio=1.5, cs_samplesPerPixel=8, cs_background=R.sky)
-    img = R.raytrace(cs, world, R.mkStdGen(4))
+    img = R.raytrace(cs, world, R.mkStdGen(4), precision=precision)
     ref = oracle_mod.render(cs, world, R.mkStdGen(4), mode=oracle_mod.RNG_PHILOX)
-    assert pixel_agreement(img, ref) >= 0.98
-    np.testing.assert_allclose(img.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=5e-3)
+    assert_parity(img, ref, precision, 0.98, _floor()["cornell"], "moving", 8, 1.0)
 
 
-def test_device_scene_async_and_encode8(gpu):
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_device_scene_async_and_encode8_bit_exact(gpu, precision):
     torch = gpu
     from raytrace_amd import _lib
     cs, world, seed = scenes.cornell_box(spp=4, width=64)
     ds = R.DeviceScene(world)
-    out = torch.empty((64, 64, 3), dtype=torch.float32, device="cuda")
+    dt = torch.float64 if precision == "f64" else torch.float32
+    out = torch.empty((64, 64, 3), dtype=dt, device="cuda")
     s = torch.cuda.current_stream()
-    ds.render_async(cs, seed, out.data_ptr(), s.cuda_stream)
+    ds.render_async(cs, seed, out.data_ptr(), s.cuda_stream, precision=precision)
     torch.cuda.synchronize()
-    np.testing.assert_array_equal(out.cpu().numpy(), R.raytrace(cs, world, seed))
-    codes = torch.empty((64, 64, 3), dtype=torch.uint8, device="cuda")
+    np.testing.assert_array_equal(out.cpu().numpy(), R.raytrace(cs, world, seed, precision=precision))
+    # the render plus every code boundary (the host thresholds and their neighbours), NaN, +-inf,
+    # negative and > 1 values: the device codes equal the host encoder's bit for bit
+    x = np.linspace(0.0, 1.0, 4097)
+    special = np.array([np.nan, np.inf, -np.inf, -1.0, -0.0, 0.0, 2.0, 1.0, 0.0031308, 0.04045, 1e-300])
+    edges = []
+    for enc in ("srgb", "sqrt"):
+        for k in range(1, 256):  # bisect each code boundary on the host encoder
+            lo, hi = 0.0, 1.0
+            for _ in range(80):
+                mid = 0.5 * (lo + hi)
+                if R.encode8(np.array([mid]), enc)[0] >= k:
+                    hi = mid
+                else:
+                    lo = mid
+            edges += [lo, hi, np.nextafter(hi, 2.0), np.nextafter(lo, -1.0)]
+    vals = np.concatenate([out.cpu().numpy().astype(np.float64).ravel(), x, special, np.array(edges)])
+    if precision == "f32":
+        vals = vals.astype(np.float32)
+    dev = torch.from_numpy(np.ascontiguousarray(vals)).cuda()
+    codes = torch.empty(vals.shape, dtype=torch.uint8, device="cuda")
     for enc, name in [(0, "srgb"), (1, "sqrt")]:
-        _lib.check(_lib.load().rt_encode8_async(ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(codes.data_ptr()),
-                                                out.numel(), enc, ctypes.c_void_p(s.cuda_stream)))
+        _lib.check(_lib.load().rt_encode8_async(ctypes.c_void_p(dev.data_ptr()), 1 if precision == "f64" else 0,
+                                                ctypes.c_void_p(codes.data_ptr()), vals.size, enc,
+                                                ctypes.c_void_p(s.cuda_stream)))
         torch.cuda.synchronize()
-        host = R.encode8(out.cpu().numpy(), name)
-        assert np.abs(codes.cpu().numpy().astype(int) - host.astype(int)).max() <= 1
+        np.testing.assert_array_equal(codes.cpu().numpy(), R.encode8(vals, name))
     ds.close()
 
 
@@ -302,3 +419,5 @@ def test_invalid_inputs_raise(gpu):
         R.raytrace(cs, R.lambertian(R.solidTexture(lambda p: p)) << R.sphere((0, 0, 0), 1), seed)
     with pytest.raises(R.RtInvalid):
         R.raytrace(cs.replace(cs_samplesPerPixel=0), world, seed)
+    with pytest.raises(R.RtInvalid):
+        R.raytrace(cs, world, seed, devices=[0, 99])
