@@ -29,7 +29,9 @@ Extra fields: `roofline` — the physical ceiling of the render kernel: VALU ins
 samples this launch renders, / its device time per frame from HIP events over the timed region —
 `kernel_ms`, the span of the timed frames / frames; `launch_ms` is the average single-launch
 duration, longer when two launches overlap — against 256 CUs x 4 SIMDs x one wave64 VALU
-instruction per 2 cycles at 2.4 GHz; frac <= 1 by construction), with `traffic` = the PMC-measured
+instruction per 2 cycles at 2.4 GHz; frac <= 1 by construction; `mix_frac` = the time the VALUs
+need for the launch's measured instruction mix at the per-class throughput a full chip sustains
+(tools/microbench/valu_rates.hip, profiles/r2/valu_rates.json) / the kernel time), with `traffic` = the PMC-measured
 HBM bytes per launch and `hbm_gbs` = traffic / kernel time beside it, and the SURVEY.md §8(d)
 algorithmic bytes (the REFERENCE's traversal: every Cornell quad tested every segment) kept as a
 labelled `reference_traversal_bytes` figure — it exceeds HBM peak because the kernel reads its
@@ -126,6 +128,30 @@ def pmc_record(config, precision):
     return d.get(f"{config}/{precision}")
 
 
+# instruction class (PMC SQ_INSTS_VALU_<class>) -> the microbenchmark's throughput key
+MIX_RATE_KEYS = {"fma_f64": "fma_f64", "mul_f64": "mul_f64", "add_f64": "add_f64", "trans_f64": "rcp_f64",
+                 "trans_f32": "sin_f32", "int64": "mad_u64_u32_plus"}
+
+
+def mix_time_s(mix, total):
+    """Seconds the chip's VALUs need for `total` wave-instructions of class mix `mix` at the
+    measured per-class throughput (profiles/r2/valu_rates.json); classes not listed (f32 / int32
+    arithmetic, moves, selects, compares) at the v_fma_f32 rate."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "r2", "valu_rates.json")) as f:
+            rates = json.load(f)
+    except Exception:
+        return None
+    if not mix:
+        return None
+    t, used = 0.0, 0.0
+    for cls, key in MIX_RATE_KEYS.items():
+        n = mix.get(cls, 0.0)
+        t += n / (rates[key] * 1e9)
+        used += n
+    return t + max(0.0, total - used) / (rates["fma_f32"] * 1e9)
+
+
 def roofline_of(config, precision, kernel_ms, launch_ms, share, samples_per_launch, concurrent):
     """The physical roofline of the render kernel: VALU issue from the committed PMC counts (full
     frame, scaled by `share` = the fraction of the frame's samples this launch renders), measured
@@ -150,6 +176,11 @@ def roofline_of(config, precision, kernel_ms, launch_ms, share, samples_per_laun
     r.update(achieved=round(ach, 1), frac=round(ach / VALU_PEAK_GINST, 4),
              valu_insts_per_launch=round(valu), lane_utilisation=round(d["lane_utilisation"], 4),
              pmc_round=d.get("round"), pmc_share_scale=round(share, 6))
+    mt = mix_time_s(d.get("valu_mix_per_launch"), d["valu_insts_per_launch"])
+    if mt is not None:
+        # the time the VALU needs for this launch's instruction mix at the measured per-class
+        # throughput of a full chip (tools/microbench/valu_rates.hip), over the measured time
+        r["mix_frac"] = round(mt * share / (kernel_ms * 1e-3), 4)
     if d.get("hbm_bytes_per_launch") is not None:
         traffic = d["hbm_bytes_per_launch"] * share
         r.update(traffic=round(traffic), hbm_gbs=round(traffic / (kernel_ms * 1e-3) / 1e9, 1),

@@ -135,23 +135,33 @@ struct AtomicCommit {
 #ifndef RT_WAVES_BVH_LITE
 #define RT_WAVES_BVH_LITE 5
 #endif
-// binary64: every real is a register pair, so the same code needs about twice the VGPRs
+// binary64: every real is a register pair, so the same code needs about twice the VGPRs; the
+// lightest instantiations (constant textures, no media, no materials beyond the diffuse ones)
+// keep more waves
+#ifndef RT_WAVES64_FLAT_LITE
+#define RT_WAVES64_FLAT_LITE 4
+#endif
 #ifndef RT_WAVES64_FLAT
-#define RT_WAVES64_FLAT 4
+#define RT_WAVES64_FLAT 2  // readme f64 0.87 -> 0.78 ms at 2 (4: 1.31); the BVH kernels keep 3 (2: demo1 +23 %, pawn+fog +17 %)
+#endif
+#ifndef RT_WAVES64_BVH_LITE
+#define RT_WAVES64_BVH_LITE 3
 #endif
 #ifndef RT_WAVES64_BVH
 #define RT_WAVES64_BVH 3
 #endif
 #if RT_F64
-#define RT_WAVES_OF(kVar, kTex, kMedia) ((kVar) == RT_VAR_FLAT ? RT_WAVES64_FLAT : RT_WAVES64_BVH)
+#define RT_WAVES_OF(kVar, kTex, kMedia, kMats)                                                     \
+  ((kVar) == RT_VAR_FLAT ? ((kTex) == 0 && !(kMedia) && !(kMats) ? RT_WAVES64_FLAT_LITE : RT_WAVES64_FLAT) \
+                         : ((kTex) == 0 && !(kMedia) && !(kMats) ? RT_WAVES64_BVH_LITE : RT_WAVES64_BVH))
 #else
-#define RT_WAVES_OF(kVar, kTex, kMedia)                                                                  \
+#define RT_WAVES_OF(kVar, kTex, kMedia, kMats)                                                           \
   ((kVar) == RT_VAR_FLAT ? ((kTex) == 2 ? RT_WAVES_FLAT_NOISE : (kTex) == 0 ? RT_WAVES_FLAT_TEX0 : RT_WAVES_FLAT) \
                          : ((kTex) == 0 && !(kMedia) ? RT_WAVES_BVH_LITE : RT_WAVES_BVH))
 #endif
 template <int kVar, int kTex, bool kMedia, bool kMats>
 __global__ __launch_bounds__(kVar == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH)
-__attribute__((amdgpu_waves_per_eu(RT_WAVES_OF(kVar, kTex, kMedia))))
+__attribute__((amdgpu_waves_per_eu(RT_WAVES_OF(kVar, kTex, kMedia, kMats))))
 void rt_render_kernel(KernelParams P) {
   extern __shared__ int smem[];
   // every wave starts with a static pool (its wave index x RT_POOL): at launch all resident waves
