@@ -208,6 +208,9 @@ typedef struct rt_device_scene rt_device_scene;   /* opaque, device-resident sce
 
 int rt_abi_version(void);
 const char* rt_last_error(void);   /* thread-local message of the last failing call */
+/* number of visible HIP devices (>= 1), or RT_E_HIP when there is none — what a caller puts in a
+ * device list to render on every GPU of the node (rt_exec.devices) */
+int rt_device_count(void);
 
 /* image height for a width and aspect ratio: round (w / aspect), banker's rounding (Ray.hs:123) */
 int rt_image_height(const rt_camera_settings* cs);

@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("RT_AMD_LIB") or os.path.join(HERE, "_lib", "librt_amd
 
 RT_OK, RT_E_GENERIC, RT_E_INVALID, RT_E_UNSUPPORTED, RT_E_HIP, RT_E_STACK = 0, -1, -2, -3, -4, -5
 
-EXPORTED = ["rt_abi_version", "rt_last_error", "rt_image_height", "rt_shard_rows", "rt_shard_row", "rt_render",
+EXPORTED = ["rt_abi_version", "rt_last_error", "rt_device_count", "rt_image_height", "rt_shard_rows", "rt_shard_row", "rt_render",
             "rt_scene_create", "rt_scene_destroy", "rt_scene_stats", "rt_render_async", "rt_encode8_async"]
 
 

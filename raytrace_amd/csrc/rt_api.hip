@@ -174,6 +174,12 @@ int rt_abi_version(void) { return RT_ABI_VERSION; }
 
 const char* rt_last_error(void) { return g_err.c_str(); }
 
+int rt_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RT_E_HIP, "no HIP device");
+  return n;
+}
+
 int rt_image_height(const rt_camera_settings* cs) {
   if (!cs) return fail(RT_E_INVALID, "null camera settings");
   int h = rt_host_image_height(cs);

@@ -148,3 +148,27 @@ def test_device_list_validation_before_device():
     assert L.rt_render(ctypes.byref(c), ctypes.byref(sc), 1, ctypes.byref(ex), out.ctypes.data, None) == _lib.RT_E_INVALID
     with pytest.raises(ValueError):
         _lib.exec_struct(precision="bf16")
+
+
+def test_haskell_binding_offsets_match_header():
+    """hs/Graphics/Ray/Device.hs marshals the rt.h records by byte offset (GHC is absent here, so
+    it cannot be compiled): every `-- LAYOUT <struct>[.<field>] <bytes>` line it declares must
+    equal the C compiler's sizeof / offsetof, and its foreign imports must name exported symbols."""
+    hs = open(os.path.join(ROOT, "hs", "Graphics", "Ray", "Device.hs")).read()
+    decl = re.findall(r"^-- LAYOUT (\w+)(?:\.(\w+))? (\d+)$", hs, flags=re.M)
+    assert len(decl) >= 30
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "rt.h"', "int main(void) {"]
+    for st, field, _ in decl:
+        expr = f"offsetof({st}, {field})" if field else f"sizeof({st})"
+        lines.append(f'  printf("%zu\\n", {expr});')
+    lines += ["  return 0;", "}"]
+    with tempfile.TemporaryDirectory() as d:
+        src, exe = os.path.join(d, "hs_layout.c"), os.path.join(d, "hs_layout")
+        open(src, "w").write("\n".join(lines) + "\n")
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", exe, src], check=True)
+        got = [int(x) for x in subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()]
+    for (st, field, want), g in zip(decl, got):
+        assert int(want) == g, (st, field, want, g)
+    imports = re.findall(r'foreign import ccall (?:safe|unsafe) "(\w+)"', hs)
+    assert set(imports) <= set(_lib.EXPORTED) and "rt_render" in imports
+    assert 'error "' not in hs  # no unimplemented stubs
