@@ -12,7 +12,7 @@ import sys
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "librt_oracle.so")
+LIB_PATH = os.environ.get("RT_ORACLE_LIB") or os.path.join(HERE, "_build", "librt_oracle.so")  # env: sanitizer builds (tests/test_sanitizers.py)
 
 RNG_SPLITMIX = 0
 RNG_PHILOX = 1

@@ -254,7 +254,11 @@ constexpr real kPi = RL(3.14159265358979323846);
 constexpr real kTmin = RL(0.0001);  // Ray.hs:178
 constexpr real kInf = RT_HUGE;
 
+#ifdef RT_HOST_EMU
+struct alignas(16) v4 {  // the host emulator's std::vector buffers guarantee 16 B
+#else
 struct alignas(4 * sizeof(real)) v4 {
+#endif
   real x, y, z, w;
 };
 struct alignas(16) v4f {  // BVH node data (float in both precisions)
@@ -409,7 +413,15 @@ struct PrimRec {
   v4 a, b, c, e;
 };
 RT_FN PrimRec ld_rec(cfp pr) { return PrimRec{ldc4(pr), ldc4(pr + 4), ldc4(pr + 8), ldc4(pr + 12)}; }
-struct alignas(16 * sizeof(real)) PrimRec64 {  // one record: 64 B (float) / 128 B (binary64)
+// one record: 64 B (float) / 128 B (binary64), record-aligned in device memory (hipMalloc bases
+// are 256-B aligned) so a wave-uniform record is one wide scalar load; the host emulator's
+// std::vector buffers only guarantee 16 B
+#ifdef RT_HOST_EMU
+#define RT_REC_ALIGN 16
+#else
+#define RT_REC_ALIGN (16 * sizeof(real))
+#endif
+struct alignas(RT_REC_ALIGN) PrimRec64 {
   real f[16];
 };
 RT_FN PrimRec ld_rec64(const RT_CAS PrimRec64* p) {

@@ -6,7 +6,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "_build", "librt_emu.so")
+LIB = os.environ.get("RT_EMU_LIB") or os.path.join(HERE, "_build", "librt_emu.so")  # env: sanitizer builds (tests/test_sanitizers.py)
 _lib = None
 
 
