@@ -429,7 +429,7 @@ foreign import ccall safe "rt_device_count"
 -- LAYOUT rt_perlin.grad 3072
 -- LAYOUT rt_motion 48
 -- LAYOUT rt_uvframe 72
--- LAYOUT rt_scene 120
+-- LAYOUT rt_scene 136
 -- LAYOUT rt_scene.prims 8
 -- LAYOUT rt_scene.media 24
 -- LAYOUT rt_scene.materials 40
@@ -438,6 +438,10 @@ foreign import ccall safe "rt_device_count"
 -- LAYOUT rt_scene.uvframes 88
 -- LAYOUT rt_scene.texels 104
 -- LAYOUT rt_scene.perlin 112
+-- LAYOUT rt_scene.n_instances 120
+-- LAYOUT rt_scene.instances 128
+-- LAYOUT rt_instance 112
+-- LAYOUT rt_instance.m 16
 -- LAYOUT rt_redirect_target 80
 -- LAYOUT rt_camera_settings 184
 -- LAYOUT rt_camera_settings.image_width 88
@@ -478,7 +482,7 @@ withFlatScene Flat{..} k =
      allocaBytes (max 1 (72 * length frames)) $ \pf ->
      allocaBytes (max 1 (12 * length texels)) $ \ptx ->
      allocaBytes 9216 $ \pper ->
-     allocaBytes 120 $ \sc -> do
+     allocaBytes 136 $ \sc -> do
        fillBytes pp 0 (152 * length prims)
        forM_ (zip [0 ..] prims) $ \(i, Prim{..}) -> do
          let b = pp `plusPtr` (152 * i)
@@ -520,7 +524,7 @@ withFlatScene Flat{..} k =
            forM_ [0 .. 255] $ \j -> pokeI32 pper (4 * (256 * a + j)) (fromIntegral (A.index' perm j))
          let grads = evalState (mapM (const randomUnitVector) [1 .. 256 :: Int]) (mkStdGen 666) :: [V3 Double]
          forM_ (zip [0 ..] grads) $ \(j, g) -> pokeDoubles pper (3072 + 24 * j) (v3l g)
-       fillBytes sc 0 120
+       fillBytes sc 0 136  -- n_instances = 0: this flatten bakes every transform into world space
        let arr off n p = pokeI32 sc off (fromIntegral n) >> pokeByteOff sc (off + 8) (if n > 0 then castPtr p else nullPtr :: Ptr ())
        arr 0 (length prims) pp
        arr 16 (length media) pm

@@ -80,15 +80,22 @@ extern "C" {
 #define RT_BG_CONST 0         /* c0 */
 #define RT_BG_LERP_Y 1        /* (1 - a) c0 + a c1, a = 0.5 (dir.y + 1)  (`sky`, `grayFade`) */
 
-/* One leaf surface.  Ray.hs/Geometry.hs semantics; all coordinates in world space. */
+/* rt_prim.set of the object-space leaves of instanced object b (rt_instance.blas == b) */
+#define RT_SET_BLAS(b) (-1 - (b))
+
+/* One leaf surface.  Ray.hs/Geometry.hs semantics; coordinates in world space, or in the
+ * object space of an instanced object (set RT_SET_BLAS(b)). */
 typedef struct rt_prim {
   int32_t kind;      /* RT_PRIM_* */
-  int32_t material;  /* index into rt_scene.materials (ignored for medium boundaries)          */
-  int32_t set;       /* 0 = visible surface; k >= 1 = boundary of rt_scene.media[k-1]         */
+  int32_t material;  /* index into rt_scene.materials (ignored for medium boundaries; -1 allowed
+                        for an instanced object's leaves when every instance of it has one)   */
+  int32_t set;       /* 0 = visible surface; k >= 1 = boundary of rt_scene.media[k-1];
+                        RT_SET_BLAS(b) = a leaf of instanced object b (object space)          */
   int32_t motion;    /* -1 or index into rt_scene.motions (`moving`, Geometry.hs:449-456)      */
   int32_t gid;       /* geometric identity: the same source leaf under the same transform has
                         the same gid in every set (used to skip self-intersection)          */
-  int32_t order;     /* depth-first position of the leaf in the caller's tree (tie-break)     */
+  int32_t order;     /* depth-first position of the leaf in the caller's tree (tie-break);
+                        for an instanced object's leaf: its position inside the object        */
   int32_t uvframe;   /* -1 or index into rt_scene.uvframes: rotation R^T for sphereUV         */
   int32_t pad;
   double p[9];       /* sphere: center[3], radius, -; plane: q[3], u[3], v[3]                 */
@@ -130,6 +137,20 @@ typedef struct rt_uvframe {
   double r[9];           /* row-major 3x3: object-space normal = r * world-space normal */
 } rt_uvframe;
 
+/* Two-level instancing of `transform` (Geometry.hs:382-391): one placement of an instanced
+ * object (the leaves with set RT_SET_BLAS(blas), traced in object space under its own BVH).
+ * The world ray enters the object through the inverse of the rigid transform m; t is unchanged
+ * (rigid), hit points / normals go back through m.  The instance's leaves take depth-first
+ * orders order .. order + (leaves of the object) - 1 in the tie-break. */
+typedef struct rt_instance {
+  int32_t blas;      /* instanced object */
+  int32_t material;  /* material of every surface of this placement (the outermost `<$`), or -1:
+                        the leaves' own materials */
+  int32_t order;     /* depth-first order of the object's first leaf in the caller's tree */
+  int32_t pad;
+  double m[12];      /* object -> world, row-major 3 x 4, rigid (R^T R = I) */
+} rt_instance;
+
 typedef struct rt_scene {
   int32_t n_prims;      const rt_prim* prims;
   int32_t n_media;      const rt_medium* media;
@@ -139,6 +160,7 @@ typedef struct rt_scene {
   int32_t n_uvframes;   const rt_uvframe* uvframes;
   int32_t n_texels;     const float* texels;      /* image textures' linear RGB, 3 floats each */
   const rt_perlin* perlin;                        /* required by noise / marble textures   */
+  int32_t n_instances;  const rt_instance* instances;  /* two-level instancing (may be 0)  */
 } rt_scene;
 
 typedef struct rt_redirect_target {   /* cs_redirectTargets element (p, q, u, v) */

@@ -46,6 +46,7 @@ class RtScene(ctypes.Structure):
         ("n_uvframes", ctypes.c_int32), ("uvframes", ctypes.c_void_p),
         ("n_texels", ctypes.c_int32), ("texels", ctypes.c_void_p),
         ("perlin", ctypes.c_void_p),
+        ("n_instances", ctypes.c_int32), ("instances", ctypes.c_void_p),
     ]
 
 
@@ -159,6 +160,8 @@ def scene_struct(flat):
     texels = np.ascontiguousarray(flat.texels, dtype=np.float32).reshape(-1, 3)
     s.n_texels, s.texels = len(texels), ptr(texels)
     s.perlin = ptr(flat.perlin) if flat.perlin is not None else None
+    inst = getattr(flat, "instances", None)
+    s.n_instances, s.instances = (len(inst), ptr(inst)) if inst is not None and len(inst) else (0, None)
     s._keep = keep
     return s
 

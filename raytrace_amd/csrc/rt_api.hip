@@ -59,6 +59,7 @@ struct DevArrays {
   R* perlin_grad = nullptr;
   R* flat_recs = nullptr;
   DevBoxT<R>* boxes = nullptr;
+  DevInstanceT<R>* instances = nullptr;
   DevMediumT<R> media[RT_MAX_MEDIA];
   int resident_blocks = 0;  // render-kernel workgroups resident on the device (occupancy query)
   int upload(const HostArraysT<R>& H) {
@@ -67,14 +68,16 @@ struct DevArrays {
         (rc = ::upload(&prim_uv, H.prim_uv)) || (rc = ::upload(&mats, H.mats)) || (rc = ::upload(&texs, H.texs)) ||
         (rc = ::upload(&motions, H.motions)) || (rc = ::upload(&uvframes, H.uvframes)) ||
         (rc = ::upload(&flat_recs, H.flat_recs)) || (rc = ::upload(&boxes, H.boxes)) ||
-        (rc = ::upload(&texels, H.texels)) || (rc = ::upload(&perlin_grad, H.perlin_grad)))
+        (rc = ::upload(&texels, H.texels)) || (rc = ::upload(&perlin_grad, H.perlin_grad)) ||
+        (rc = ::upload(&instances, H.instances)))
       return rc;
     for (int k = 0; k < RT_MAX_MEDIA; ++k) media[k] = H.media[k];
     return RT_OK;
   }
   void release() {
     for (void* p : {(void*)prims, (void*)prim_shade, (void*)prim_uv, (void*)mats, (void*)texs, (void*)motions,
-                    (void*)uvframes, (void*)texels, (void*)perlin_grad, (void*)flat_recs, (void*)boxes})
+                    (void*)uvframes, (void*)texels, (void*)perlin_grad, (void*)flat_recs, (void*)boxes,
+                    (void*)instances})
       (void)hipFree(p);
   }
 };
@@ -131,6 +134,7 @@ int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_
   P.perlin_grad = A.perlin_grad;
   P.flat_recs = A.flat_recs;
   P.boxes = A.boxes;
+  P.instances = A.instances;
   P.status = s->status;
   P.out = d_out;
   P.surface_root = s->surface_root;
@@ -239,7 +243,7 @@ int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
   s->n_prims = H.n_prims;
   s->max_depth = H.max_depth;
   s->stack_depth = H.max_depth > 1 ? H.max_depth : 1;
-  s->variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex);
+  s->variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex, H.n_instances > 0);
   if ((s->variant & RT_VAR_BASE) != RT_VAR_FLAT) {
     // stage as many top (breadth-first) surface nodes as fit beside the stacks in the per-
     // workgroup budget; env RT_AMD_LDS_NODES caps it (0 disables, for experiments)

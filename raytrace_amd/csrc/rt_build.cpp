@@ -311,6 +311,20 @@ void fill_records(const rt_scene* sc, const std::vector<int>& order, const std::
       for (int c = 0; c < 3; ++c) A.uvframes[12 * (size_t)i + 4 * r + c] = (R)sc->uvframes[i].r[3 * r + c];
 }
 
+template <class R>
+void fill_instances(const rt_scene* sc, const std::vector<int>& blas_root, HostArraysT<R>& A) {
+  A.instances.assign(sc->n_instances, DevInstanceT<R>{});
+  for (int k = 0; k < sc->n_instances; ++k) {
+    const rt_instance& I = sc->instances[k];
+    DevInstanceT<R>& d = A.instances[k];
+    for (int a = 0; a < 12; ++a) d.m[a] = (R)I.m[a];
+    d.root = blas_root[I.blas];
+    d.material = I.material;
+    d.order = I.order;
+    d.pad = 0;
+  }
+}
+
 }  // namespace
 
 int rt_host_image_height(const rt_camera_settings* cs) {
@@ -381,13 +395,34 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     if (m.material < 0 || m.material >= sc->n_materials) return fail(err, RT_E_INVALID, "medium %d: bad material", k);
   }
   const int n_sets = 1 + sc->n_media;
-  std::vector<std::vector<BuildPrim>> sets(n_sets);
+  // two-level instancing: instanced objects (prims with set RT_SET_BLAS(b)) and their placements
+  if (sc->n_instances < 0 || (sc->n_instances && !sc->instances)) return fail(err, RT_E_INVALID, "bad instance array");
+  int n_blas = 0;
+  for (int i = 0; i < sc->n_prims; ++i)
+    if (sc->prims[i].set < 0) n_blas = std::max(n_blas, -sc->prims[i].set);
+  for (int k = 0; k < sc->n_instances; ++k) {
+    const rt_instance& I = sc->instances[k];
+    if (I.blas < 0 || I.blas >= n_blas) return fail(err, RT_E_INVALID, "instance %d: object %d has no leaves", k, I.blas);
+    if (I.material < -1 || I.material >= sc->n_materials) return fail(err, RT_E_INVALID, "instance %d: bad material", k);
+    if (!finite_n(I.m, 12)) return fail(err, RT_E_INVALID, "instance %d: non-finite transform", k);
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) {
+        const double d = I.m[a] * I.m[b] + I.m[4 + a] * I.m[4 + b] + I.m[8 + a] * I.m[8 + b];
+        if (std::fabs(d - (a == b ? 1.0 : 0.0)) > 1e-9)
+          return fail(err, RT_E_UNSUPPORTED, "instance %d: transform is not rigid (Geometry.hs:379-381)", k);
+      }
+  }
+  std::vector<std::vector<BuildPrim>> sets(n_sets), blas_sets(n_blas);
+  std::vector<char> blas_all_mats(n_blas, 1);
   for (int i = 0; i < sc->n_prims; ++i) {
     const rt_prim& p = sc->prims[i];
     if (p.kind < RT_PRIM_SPHERE || p.kind > RT_PRIM_TRIANGLE) return fail(err, RT_E_INVALID, "prim %d: bad kind", i);
-    if (p.set < 0 || p.set >= n_sets) return fail(err, RT_E_INVALID, "prim %d: bad set %d", i, p.set);
+    if (p.set >= n_sets) return fail(err, RT_E_INVALID, "prim %d: bad set %d", i, p.set);
     if (p.set == 0 && (p.material < 0 || p.material >= sc->n_materials))
       return fail(err, RT_E_INVALID, "prim %d: surface without a valid material", i);
+    if (p.set < 0 && (p.material < -1 || p.material >= sc->n_materials))
+      return fail(err, RT_E_INVALID, "prim %d: bad material", i);
+    if (p.set < 0 && p.material < 0) blas_all_mats[-1 - p.set] = 0;
     if (p.motion >= sc->n_motions || p.uvframe >= sc->n_uvframes)
       return fail(err, RT_E_INVALID, "prim %d: bad motion/uvframe index", i);
     if (!finite_n(p.p, p.kind == RT_PRIM_SPHERE ? 4 : 9))
@@ -421,16 +456,49 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
         bp.hi[a] = std::fmax(hi + m.v0[a], hi + m.v1[a]);
       }
     }
-    sets[p.set].push_back(bp);
+    if (p.set < 0)
+      blas_sets[-1 - p.set].push_back(bp);
+    else
+      sets[p.set].push_back(bp);
   }
   for (int k = 0; k < sc->n_media; ++k)
     if (sets[k + 1].empty()) return fail(err, RT_E_INVALID, "medium %d has an empty boundary", k);
+  // every placement is one item of the surface set, boxed by its object's box under the transform
+  for (int k = 0; k < sc->n_instances; ++k) {
+    const rt_instance& I = sc->instances[k];
+    if (blas_sets[I.blas].empty()) return fail(err, RT_E_INVALID, "instance %d: object %d has no leaves", k, I.blas);
+    if (I.material < 0 && !blas_all_mats[I.blas])
+      return fail(err, RT_E_INVALID, "instance %d: a leaf of object %d has no material", k, I.blas);
+    double olo[3] = {INFINITY, INFINITY, INFINITY}, ohi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (const BuildPrim& b : blas_sets[I.blas])
+      for (int a = 0; a < 3; ++a) {
+        olo[a] = std::min(olo[a], b.lo[a]);
+        ohi[a] = std::max(ohi[a], b.hi[a]);
+      }
+    BuildPrim bp;
+    bp.index = -1;
+    bp.inst = k;
+    for (int a = 0; a < 3; ++a) {
+      bp.lo[a] = INFINITY;
+      bp.hi[a] = -INFINITY;
+    }
+    for (int c = 0; c < 8; ++c) {
+      const double x[3] = {(c & 1) ? ohi[0] : olo[0], (c & 2) ? ohi[1] : olo[1], (c & 4) ? ohi[2] : olo[2]};
+      for (int a = 0; a < 3; ++a) {
+        const double w = I.m[4 * a] * x[0] + I.m[4 * a + 1] * x[1] + I.m[4 * a + 2] * x[2] + I.m[4 * a + 3];
+        bp.lo[a] = std::min(bp.lo[a], w);
+        bp.hi[a] = std::max(bp.hi[a], w);
+      }
+    }
+    sets[0].push_back(bp);
+  }
 
   // media whose boundary is, leaf for leaf in depth-first order, the surface set (DevMedium)
   std::vector<int> alias(sc->n_media, 0);
   {
     std::vector<std::vector<int>> by_set(n_sets);
-    for (int i = 0; i < sc->n_prims; ++i) by_set[sc->prims[i].set].push_back(i);
+    for (int i = 0; i < sc->n_prims; ++i)
+      if (sc->prims[i].set >= 0) by_set[sc->prims[i].set].push_back(i);  // instanced objects' leaves: not a set
     for (auto& v : by_set)
       std::stable_sort(v.begin(), v.end(), [&](int x, int y) { return sc->prims[x].order < sc->prims[y].order; });
     auto same = [&](const rt_prim& a, const rt_prim& b) {
@@ -449,6 +517,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   }
   if (const char* e = std::getenv("RT_AMD_NO_ALIAS"))  // experiments: always traverse boundaries
     if (atoi(e)) std::fill(alias.begin(), alias.end(), 0);
+  if (sc->n_instances > 0) std::fill(alias.begin(), alias.end(), 0);  // the surface set also holds placements
 
   // Large-primitive prefix of the surface set (BVH scenes).  Primitives whose box is a large
   // fraction of the whole set's (the Cornell walls around a mesh, demo1's ground sphere) overlap
@@ -482,7 +551,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
       for (size_t j = 0; j < sets[0].size(); ++j) {
         const BuildPrim& b = sets[0][j];
         const double a = area(b.lo, b.hi);
-        if (sc->prims[b.index].motion < 0 && a >= frac * root_area) big.push_back({-a, (int)j});
+        if (b.inst < 0 && sc->prims[b.index].motion < 0 && a >= frac * root_area) big.push_back({-a, (int)j});
       }
       std::stable_sort(big.begin(), big.end());
       if (big.size() > RT_PREFIX_MAX) big.resize(RT_PREFIX_MAX);
@@ -515,7 +584,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
           const BuildPrim& b = sets[0][j];
           bool extreme = false;
           for (int a = 0; a < 3; ++a) extreme = extreme || b.lo[a] == l0[a] || b.hi[a] == h0[a];
-          if (taken[j] || !extreme || sc->prims[b.index].motion >= 0) continue;
+          if (taken[j] || !extreme || b.inst >= 0 || sc->prims[b.index].motion >= 0) continue;
           double l[3], h[3];
           bounds_without((int)j, l, h);
           const double a = area(l, h);
@@ -547,6 +616,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   // one BVH per set; primitives stored in leaf order, set after set (the prefix first)
   std::vector<int> order(prefix);
   std::vector<int> roots(n_sets), set_begin(n_sets + 1, 0);
+  int surface_depth = 0;
   set_begin[0] = (int)prefix.size();
   S.nodes.clear();
   S.max_depth = 0;
@@ -555,7 +625,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     // leaves of at most 2 triangles / quads (bunny-Cornell 112 -> 107 ms, pawn+fog -1.2 % against
     // 8 under the leaf-exit policy); sphere sets keep 8 (demo1 +0.6 % at 2)
     bool spheres = true;
-    for (const BuildPrim& b : sets[s]) spheres = spheres && sc->prims[b.index].kind == RT_PRIM_SPHERE;
+    for (const BuildPrim& b : sets[s]) spheres = spheres && b.inst < 0 && sc->prims[b.index].kind == RT_PRIM_SPHERE;
     int leaf_max = spheres ? RT_LEAF_MAX : 2;
     if (const char* e = std::getenv("RT_AMD_LEAF_MAX")) leaf_max = std::max(1, std::min(RT_FLAT_MAX, atoi(e)));
     rt_build_bvh(sets[s], (int)(S.nodes.size() / 16), (int)order.size(), bo, leaf_max);
@@ -564,12 +634,28 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     roots[s] = bo.root;
     S.max_depth = std::max(S.max_depth, bo.max_depth);
     set_begin[s + 1] = (int)order.size();
-    if (s == 0) S.surface_nodes = (int)(S.nodes.size() / 16);
+    if (s == 0) {
+      S.surface_nodes = (int)(S.nodes.size() / 16);
+      surface_depth = bo.max_depth;
+    }
   }
+  // instanced objects: one object-space BVH each (leaves of at most 2 primitives, as meshes),
+  // after the sets; the stack holds the world levels, the exit marker and the object's levels
+  std::vector<int> blas_root(n_blas, RT_EMPTY_ROOT);
+  int blas_depth = 0;
+  for (int b = 0; b < n_blas && sc->n_instances > 0; ++b) {
+    BvhOut bo;
+    rt_build_bvh(blas_sets[b], (int)(S.nodes.size() / 16), (int)order.size(), bo, 2);
+    S.nodes.insert(S.nodes.end(), bo.nodes.begin(), bo.nodes.end());
+    order.insert(order.end(), bo.order.begin(), bo.order.end());
+    blas_root[b] = bo.root;
+    blas_depth = std::max(blas_depth, bo.max_depth);
+  }
+  if (sc->n_instances > 0) S.max_depth = std::max(S.max_depth, surface_depth + 1 + blas_depth + 1);
   if (S.max_depth > RT_STACK_DEPTH)
     return fail(err, RT_E_STACK, "BVH depth %d exceeds the traversal stack (%d)", S.max_depth, RT_STACK_DEPTH);
   const int n = (int)order.size();
-  S.flat = S.nodes.empty() && n <= RT_LDS_PRIMS_MAX && prefix.empty();
+  S.flat = S.nodes.empty() && n <= RT_LDS_PRIMS_MAX && prefix.empty() && sc->n_instances == 0;
   if (!prefix.empty()) {  // BVH scenes: flat_sets[0] describes the surface prefix
     DevFlatSet& F = S.flat_sets[0];
     F.first = 0;
@@ -713,7 +799,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     }
   }
   S.prim_mat.assign(n, -1);
-  for (int j = 0; j < n; ++j) S.prim_mat[j] = sc->prims[order[j]].set == 0 ? sc->prims[order[j]].material : -1;
+  for (int j = 0; j < n; ++j) S.prim_mat[j] = sc->prims[order[j]].set <= 0 ? sc->prims[order[j]].material : -1;
   if (S.flat) {  // test order -> slot order for the shading arrays (prim index = slot)
     std::vector<int> mat(S.prim_mat.size());
     for (int j = 0; j < n; ++j) mat[slot_of[j]] = S.prim_mat[j];
@@ -721,6 +807,9 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   }
   fill_records(sc, order, slot_of, S.flat, boxes, box_codes, S.prim_mat, S.f32);
   fill_records(sc, order, slot_of, S.flat, boxes, box_codes, S.prim_mat, S.f64);
+  fill_instances(sc, blas_root, S.f32);
+  fill_instances(sc, blas_root, S.f64);
+  S.n_instances = sc->n_instances;
   S.n_boxes = (int)boxes.size();
   S.perlin_perm.assign(3 * 256, 0);
   if (sc->perlin)
@@ -753,8 +842,10 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   return RT_OK;
 }
 
-int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex) {
+int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, bool inst) {
   int v = flat ? RT_VAR_FLAT : RT_VAR_BVH;
+  if (inst) return RT_VAR_BVH | RT_VAR_INST | (noise ? RT_VAR_NOISE : 0) | (n_media > 0 ? RT_VAR_MEDIA : 0) |
+                   (mats ? RT_VAR_MATS : 0) | (tex ? RT_VAR_TEX : 0);  // two-level traversal: the decoupled BVH loop
   if (const char* e = std::getenv("RT_AMD_VARIANT")) {
     const int f = atoi(e);
     if (!flat && (f == RT_VAR_BVH_LOCKSTEP || f == RT_VAR_BVH)) v = f;  // flat scenes run on any variant

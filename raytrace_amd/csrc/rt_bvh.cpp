@@ -44,6 +44,12 @@ struct Builder {
   int leaf_max = RT_LEAF_MAX;
   explicit Builder(std::vector<BuildPrim>& prims) : p(prims) {}
 
+  bool has_inst(int b, int e) const {
+    for (int i = b; i < e; ++i)
+      if (p[i].inst >= 0) return true;
+    return false;
+  }
+
   Box bounds(int b, int e) const {
     Box bx;
     bx.reset();
@@ -57,7 +63,9 @@ struct Builder {
     tmp.emplace_back();
     tmp[id].box = bounds(b, e);
     int n = e - b;
-    if (n <= 2 || (depth == 0 && n <= RT_FLAT_MAX)) {  // tiny sets: one flat, coherent leaf
+    // instances are single-item leaves (RT_INST_CODE children), never mixed with primitives
+    const bool inst = has_inst(b, e);
+    if (n == 1 || (!inst && (n <= 2 || (depth == 0 && n <= RT_FLAT_MAX)))) {  // tiny sets: one flat, coherent leaf
       tmp[id].first = b;
       tmp[id].count = n;
       return id;
@@ -119,7 +127,7 @@ struct Builder {
     int mid;
     if (best_axis < 0) {
       // all centroids coincide: split in the middle of the index range
-      if (n <= leaf_max) {
+      if (n <= leaf_max && !inst) {
         tmp[id].first = b;
         tmp[id].count = n;
         return id;
@@ -127,7 +135,7 @@ struct Builder {
       mid = b + n / 2;
     } else {
       // SAH with traversal cost ~ 1 box pair ~ 1 primitive test
-      if (n <= leaf_max && leaf_cost <= node_area * 1.0 + best_cost) {
+      if (n <= leaf_max && !inst && leaf_cost <= node_area * 1.0 + best_cost) {
         tmp[id].first = b;
         tmp[id].count = n;
         return id;
@@ -167,7 +175,12 @@ void rt_build_bvh(std::vector<BuildPrim> prims, int node_base, int prim_base, Bv
   B.leaf_max = leaf_max;
   int root = B.build(0, (int)prims.size(), 0);
   out.max_depth = B.max_depth;
-  for (auto& q : prims) out.order.push_back(q.index);
+  // primitive slots skip the instance items (each is its own leaf, encoded as RT_INST_CODE)
+  std::vector<int> slot(prims.size() + 1, 0);
+  for (size_t i = 0; i < prims.size(); ++i) {
+    slot[i + 1] = slot[i] + (prims[i].inst < 0 ? 1 : 0);
+    if (prims[i].inst < 0) out.order.push_back(prims[i].index);
+  }
   // number internal nodes breadth-first: the top levels are the first nodes of the set, which
   // is what the kernel stages in LDS (KernelParams::lds_nodes)
   std::vector<int> dev_index(B.tmp.size(), -1);
@@ -184,8 +197,9 @@ void rt_build_bvh(std::vector<BuildPrim> prims, int node_base, int prim_base, Bv
   auto enc = [&](int id) -> int {
     const Node& nd = B.tmp[id];
     if (nd.left >= 0) return dev_index[id];
+    if (nd.count == 1 && prims[nd.first].inst >= 0) return RT_INST_FLAG | prims[nd.first].inst;
     // leaf: ~(first << RT_LEAF_SHIFT | count - 1); leaves hold <= RT_FLAT_MAX primitives
-    return ~(((prim_base + nd.first) << RT_LEAF_SHIFT) | (nd.count - 1));
+    return ~(((prim_base + slot[nd.first]) << RT_LEAF_SHIFT) | (nd.count - 1));
   };
   out.n_nodes = (int)internal.size();
   out.nodes.assign((size_t)out.n_nodes * 16, 0.0f);

@@ -15,12 +15,13 @@
 
 struct BuildPrim {
   double lo[3], hi[3];
-  int index;  // caller's primitive index
+  int index;      // caller's primitive index (-1 for an instance)
+  int inst = -1;  // >= 0: an instance of an instanced object (a single-item leaf, RT_INST_CODE)
 };
 
 struct BvhOut {
   std::vector<float> nodes;   // 16 floats per node (4 x float4)
-  std::vector<int> order;     // primitive order of the leaves (caller indices)
+  std::vector<int> order;     // primitive order of the leaves (caller indices; instances excluded)
   int root = 0;               // node index, leaf encoding, or RT_EMPTY_ROOT
   int max_depth = 0;          // deepest root-to-leaf path (bounds the traversal stack)
   int n_nodes = 0;

@@ -49,6 +49,11 @@
 #define RT_LDS_WG_BUDGET 31744  // BVH kernel LDS per workgroup (stack + staged nodes): 5 per CU (32512 drops to 4)
 #endif
 #define RT_EMPTY_ROOT ((int)0x80000000)
+// Two-level instancing: a BVH child RT_INST_FLAG | k enters instance k (the ray goes to object
+// space, the object's BVH is traversed); RT_INST_EXIT, pushed on entry, returns to world space.
+// Node indices stay below RT_INST_FLAG.
+#define RT_INST_FLAG 0x40000000
+#define RT_INST_EXIT 0x7FFFFFFF
 
 // render-kernel variants (rt_kernel.hip)
 #define RT_VAR_FLAT 0          // every set one flat leaf, lockstep lane loop
@@ -59,10 +64,11 @@
 #define RT_VAR_MEDIA 8         // flag: the scene has constantMedium volumes (their code compiled in)
 #define RT_VAR_MATS 16         // flag: materials beyond lightSource / pitchBlack / lambertian
 #define RT_VAR_TEX 32          // flag: some material reads a non-constant texture
+#define RT_VAR_INST 64         // flag: the scene has instances (two-level traversal; RT_VAR_BVH only)
 // workgroup size of a variant's render kernel
 inline int rt_block_of(int variant) { return (variant & RT_VAR_BASE) == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH; }
 // host choice of variant (rt_build.cpp); env RT_AMD_VARIANT overrides the base for experiments
-int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex);
+int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, bool inst = false);
 
 #define RT_KIND_MASK 3
 #define RT_FLAG_MOTION 4
@@ -170,6 +176,18 @@ struct DevTargetT {
   R pad;
 };
 
+// One placement of an instanced object (rt.h rt_instance): object -> world rigid transform,
+// the object's BVH root, the placement's material (or -1) and the depth-first order of its first
+// leaf (added to the object-space leaves' orders in the closest-hit key).
+template <class R>
+struct DevInstanceT {
+  R m[12];       // row-major 3 x 4: rotation | translation
+  int root;
+  int material;
+  int order;
+  int pad;
+};
+
 template <class R>
 struct DevCameraT {
   R center[3], top_left[3], pixel_u[3], pixel_v[3], disk_u[3], disk_v[3];
@@ -203,6 +221,7 @@ struct KernelParamsT {
   const R* perlin_grad;    // 256 gradients, 4 R each (xyz, -)
   const R* flat_recs;      // flat scenes: the test records, class-grouped (DevFlatSet ranges)
   const DevBoxT<R>* boxes; // box groups of the flat sets / the surface prefix (DevBox)
+  const DevInstanceT<R>* instances;  // two-level instancing (RT_VAR_INST)
   R* out;                  // linear RGB of the tile, R per channel
   int* status;             // device word: nonzero on stack overflow
   // persistent-lane work queue (rt_trace.h lane_loop): items = n_chunks x tile pixels
@@ -236,6 +255,7 @@ using DevMedium = DevMediumT<float>;
 using DevBox = DevBoxT<float>;
 using DevTarget = DevTargetT<float>;
 using DevCamera = DevCameraT<float>;
+using DevInstance = DevInstanceT<float>;
 using KernelParams = KernelParamsT<float>;
 using KernelParams64 = KernelParamsT<double>;
 
@@ -254,6 +274,7 @@ struct HostArraysT {
   std::vector<DevMaterialT<R>> prim_shade, mats;
   std::vector<DevTextureT<R>> texs;
   std::vector<DevBoxT<R>> boxes;  // box groups (DevBox)
+  std::vector<DevInstanceT<R>> instances;
   DevMediumT<R> media[RT_MAX_MEDIA];
 };
 struct HostScene {
@@ -273,6 +294,7 @@ struct HostScene {
   int leaf_exit_pct = 100;  // BVH traversal policy for this scene (KernelParams::leaf_exit_pct)
   int trav_exit_pct = 50;   // and its lane-loop exit (KernelParams::trav_exit_pct)
   bool full_mats = false;  // some material is not lightSource / pitchBlack / lambertian (RT_VAR_MATS)
+  int n_instances = 0;     // two-level instancing (RT_VAR_INST)
   template <class R>
   const HostArraysT<R>& arrays() const;
 };

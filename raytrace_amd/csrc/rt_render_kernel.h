@@ -159,7 +159,7 @@ struct AtomicCommit {
   ((kVar) == RT_VAR_FLAT ? ((kTex) == 2 ? RT_WAVES_FLAT_NOISE : (kTex) == 0 ? RT_WAVES_FLAT_TEX0 : RT_WAVES_FLAT) \
                          : ((kTex) == 0 && !(kMedia) ? RT_WAVES_BVH_LITE : RT_WAVES_BVH))
 #endif
-template <int kVar, int kTex, bool kMedia, bool kMats>
+template <int kVar, int kTex, bool kMedia, bool kMats, bool kInst>
 __global__ __launch_bounds__(kVar == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH)
 __attribute__((amdgpu_waves_per_eu(RT_WAVES_OF(kVar, kTex, kMedia, kMats))))
 void rt_render_kernel(KernelParams P) {
@@ -188,7 +188,7 @@ void rt_render_kernel(KernelParams P) {
     if constexpr (kVar == RT_VAR_BVH_LOCKSTEP)
       overflow = lane_loop_lockstep<false, kTex, kMedia, kMats>(P, grab, commit, W, P.prims);
     else
-      overflow = lane_loop_bvh<kTex, kMedia, kMats>(P, grab, commit, W, P.prims);
+      overflow = lane_loop_bvh<kTex, kMedia, kMats, kInst>(P, grab, commit, W, P.prims);
   }
   if (overflow) atomicOr(P.status, 1);
 }
@@ -225,26 +225,29 @@ static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
 // (inlined everywhere it raises the register allocation of every scene's kernel: the Cornell
 // box is 4.8 % faster without the unused media code)
 typedef void (*render_fn)(KernelParams);
-template <int kVar, int kTex, bool kMedia>
+template <int kVar, int kTex, bool kMedia, bool kInst>
 static render_fn render_kernel_mats(int variant) {
-  return (variant & RT_VAR_MATS) ? rt_render_kernel<kVar, kTex, kMedia, true> : rt_render_kernel<kVar, kTex, kMedia, false>;
+  return (variant & RT_VAR_MATS) ? rt_render_kernel<kVar, kTex, kMedia, true, kInst>
+                                 : rt_render_kernel<kVar, kTex, kMedia, false, kInst>;
 }
-template <int kVar, int kTex>
+template <int kVar, int kTex, bool kInst>
 static render_fn render_kernel_media(int variant) {
-  return (variant & RT_VAR_MEDIA) ? render_kernel_mats<kVar, kTex, true>(variant)
-                                  : render_kernel_mats<kVar, kTex, false>(variant);
+  return (variant & RT_VAR_MEDIA) ? render_kernel_mats<kVar, kTex, true, kInst>(variant)
+                                  : render_kernel_mats<kVar, kTex, false, kInst>(variant);
 }
-template <int kVar>
+template <int kVar, bool kInst>
 static render_fn render_kernel_flags(int variant) {
-  if (variant & RT_VAR_NOISE) return render_kernel_media<kVar, 2>(variant);
-  if (variant & RT_VAR_TEX) return render_kernel_media<kVar, 1>(variant);
-  return render_kernel_media<kVar, 0>(variant);
+  if (variant & RT_VAR_NOISE) return render_kernel_media<kVar, 2, kInst>(variant);
+  if (variant & RT_VAR_TEX) return render_kernel_media<kVar, 1, kInst>(variant);
+  return render_kernel_media<kVar, 0, kInst>(variant);
 }
+// two-level instancing (RT_VAR_INST) is compiled into the decoupled BVH kernel only
 static render_fn render_kernel_of(int variant) {
+  if (variant & RT_VAR_INST) return render_kernel_flags<RT_VAR_BVH, true>(variant);
   switch (variant & RT_VAR_BASE) {
-    case RT_VAR_FLAT: return render_kernel_flags<RT_VAR_FLAT>(variant);
-    case RT_VAR_BVH_LOCKSTEP: return render_kernel_flags<RT_VAR_BVH_LOCKSTEP>(variant);
-    default: return render_kernel_flags<RT_VAR_BVH>(variant);
+    case RT_VAR_FLAT: return render_kernel_flags<RT_VAR_FLAT, false>(variant);
+    case RT_VAR_BVH_LOCKSTEP: return render_kernel_flags<RT_VAR_BVH_LOCKSTEP, false>(variant);
+    default: return render_kernel_flags<RT_VAR_BVH, false>(variant);
   }
 }
 

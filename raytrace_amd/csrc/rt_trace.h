@@ -247,6 +247,7 @@ using DevMedium = ::DevMediumT<real>;
 using DevBox = ::DevBoxT<real>;
 using DevTarget = ::DevTargetT<real>;
 using DevCamera = ::DevCameraT<real>;
+using DevInstance = ::DevInstanceT<real>;
 
 
 
@@ -363,8 +364,15 @@ RT_FN f3 unit_vector(uint32_t a, uint32_t b) {
 struct RayCtx {
   f3 o, d, idir, oidir;
   real time;
-  int self_gid;
+  int self_gid;   // the leaf the ray leaves (skipped: FP32 robustness, rt_trace.h isect_*)
+  int self_inst;  // ... and its instance (-1: a world leaf; two-level instancing, RT_VAR_INST)
 };
+// The leaf the ray leaves: gid equal, and (instancing) the same placement of the object.
+template <bool kInst>
+RT_FN bool is_self(const RayCtx& R, int gid, int cur_inst) {
+  if constexpr (kInst) return gid == R.self_gid && cur_inst == R.self_inst;
+  return gid == R.self_gid;
+}
 
 RT_FN f3 motion_shift(const KernelParams& P, int m, real time) {
   f3 v0 = ldc3(cf(P.motions) + 8 * m), v1 = ldc3(cf(P.motions) + 8 * m + 4);
@@ -372,6 +380,25 @@ RT_FN f3 motion_shift(const KernelParams& P, int m, real time) {
 }
 
 RT_FN real safe_rcp(real d) { return RT_RCP(RABS(d) > RL(1e-20) ? d : RCOPYSIGN(RL(1e-20), d)); }
+
+// reciprocal direction and origin x reciprocal for the BVH slab tests
+RT_FN void prep_ray(RayCtx& R) {
+  R.idir = mk3(safe_rcp(R.d.x), safe_rcp(R.d.y), safe_rcp(R.d.z));
+  R.oidir = R.o * R.idir;
+}
+
+// Two-level instancing (rt_internal.h DevInstance): world -> object space through the inverse of
+// the rigid placement (R^T (p - t); t is unchanged along the ray) and object -> world normals.
+RT_FN const RT_CAS DevInstance* inst_rec(const KernelParams& P, int k) { return (const RT_CAS DevInstance*)P.instances + k; }
+RT_FN f3 inst_to_object(const RT_CAS DevInstance* I, f3 v, bool point) {
+  if (point) v = v - mk3(I->m[3], I->m[7], I->m[11]);
+  return mk3(I->m[0] * v.x + I->m[4] * v.y + I->m[8] * v.z, I->m[1] * v.x + I->m[5] * v.y + I->m[9] * v.z,
+             I->m[2] * v.x + I->m[6] * v.y + I->m[10] * v.z);
+}
+RT_FN f3 inst_rotate(const RT_CAS DevInstance* I, f3 v) {
+  return mk3(I->m[0] * v.x + I->m[1] * v.y + I->m[2] * v.z, I->m[4] * v.x + I->m[5] * v.y + I->m[6] * v.z,
+             I->m[8] * v.x + I->m[9] * v.y + I->m[10] * v.z);
+}
 
 // Closest hit so far, keyed by (t, depth-first order): smaller t wins, ties go to the earlier
 // leaf (Geometry.hs:340-361).  Float kernels pack the key into 64 bits, (bits of t) << 32 |
@@ -383,12 +410,14 @@ struct Closest {
   real t;
   int ord;
   int prim;
+  int inst;  // the instance of the winning leaf (-1: world)
 };
 #else
 struct Closest {
   real t;
   unsigned long long key;
   int prim;
+  int inst;  // the instance of the winning leaf (-1: world)
 };
 #endif
 // Per-lane traversal resources: the lane's stack (stack[k * stride]) and the workgroup's LDS copy
@@ -399,9 +428,9 @@ struct Trav {
   const v4f* lds_nodes;
 };
 #if RT_F64
-RT_FN Closest no_hit() { return Closest{kInf, 0, -1}; }
+RT_FN Closest no_hit() { return Closest{kInf, 0, -1, -1}; }
 #else
-RT_FN Closest no_hit() { return Closest{kInf, 0x7f80000000000000ull, -1}; }
+RT_FN Closest no_hit() { return Closest{kInf, 0x7f80000000000000ull, -1, -1}; }
 RT_FN unsigned long long hit_key(real t, int ord) {
   return ((unsigned long long)(unsigned)RT_F2I(t) << 32) | (unsigned)ord;
 }
@@ -476,13 +505,14 @@ RT_FN void isect_plane(const PrimRec& r, f3 o, const RayCtx& R, real tmin_up, bo
   q = self ? -RL(1.0) : RMIN(m1, m2);
 }
 // kKeyOnly (flat sets): only the key is tracked; t and the primitive follow from it afterwards
-template <bool kKeyOnly>
-RT_FN void consider(Closest& C, real t, real q, int ord, int pi) {
+template <bool kKeyOnly, bool kInst = false>
+RT_FN void consider(Closest& C, real t, real q, int ord, int pi, int inst = -1) {
 #if RT_F64
   const bool take = q >= RL(0.0) && (t < C.t || (t == C.t && ord < C.ord));
   C.t = take ? t : C.t;
   C.ord = take ? ord : C.ord;
   if constexpr (!kKeyOnly) C.prim = take ? pi : C.prim;
+  if constexpr (kInst) C.inst = take ? inst : C.inst;
 #else
   const real tc = q >= RL(0.0) ? t : RT_NAN;
   const unsigned long long key = hit_key(tc, ord);
@@ -492,19 +522,21 @@ RT_FN void consider(Closest& C, real t, real q, int ord, int pi) {
     C.t = take ? tc : C.t;
     C.prim = take ? pi : C.prim;
   }
+  if constexpr (kInst) C.inst = take ? inst : C.inst;
 #endif
 }
 
 // Any primitive record against the open interval (tmin, C.t).  When the record is wave-uniform
 // (flat sets) it sits in SGPRs and the kind / motion tests are scalar branches.
-template <bool kKeyOnly = false>
+// kInst: the leaf may belong to instance cur_inst (its key order is offset by ord_base).
+template <bool kKeyOnly = false, bool kInst = false>
 RT_FN void test_rec(const KernelParams& P, const PrimRec& r, int pi, const RayCtx& R, real tmin, real tmin_up,
-                    Closest& C) {
+                    Closest& C, int cur_inst = -1, int ord_base = 0) {
   RT_COUNT(1);
   const int kf = RT_R2I(r.a.w);
   f3 o = R.o;
   if (kf & RT_FLAG_MOTION) o = o - motion_shift(P, RT_R2I(r.e.w), R.time);
-  const bool self = RT_R2I(r.b.w) == R.self_gid;
+  const bool self = is_self<kInst>(R, RT_R2I(r.b.w), cur_inst);
   real t, q;
   if ((kf & RT_KIND_MASK) == 0)
     isect_sphere(r, o, R, tmin, tmin_up, self, t, q);
@@ -514,20 +546,20 @@ RT_FN void test_rec(const KernelParams& P, const PrimRec& r, int pi, const RayCt
     isect_plane<1>(r, o, R, tmin_up, self, t, q);
   else
     isect_plane<0>(r, o, R, tmin_up, self, t, q);
-  consider<kKeyOnly>(C, t, q, RT_R2I(r.c.w), pi);
+  consider<kKeyOnly, kInst>(C, t, q, RT_R2I(r.c.w) + ord_base, pi, cur_inst);
 }
 
 // A static primitive of a known kind (flat sets are grouped by class: rt_build.cpp).
-template <int kKind, bool kKeyOnly = true>
+template <int kKind, bool kKeyOnly = true, bool kInst = false>
 RT_FN void test_static(const PrimRec& r, const RayCtx& R, real tmin, real tmin_up, Closest& C, int pi = 0) {
   RT_COUNT(1);
-  const bool self = RT_R2I(r.b.w) == R.self_gid;
+  const bool self = is_self<kInst>(R, RT_R2I(r.b.w), -1);  // a world leaf
   real t, q;
   if constexpr (kKind == RT_PRIM_CLASS_SPHERE)
     isect_sphere(r, R.o, R, tmin, tmin_up, self, t, q);
   else
     isect_plane<kKind == RT_PRIM_CLASS_QUAD ? 1 : 0>(r, R.o, R, tmin_up, self, t, q);
-  consider<kKeyOnly>(C, t, q, RT_R2I(r.c.w), pi);
+  consider<kKeyOnly, kInst>(C, t, q, RT_R2I(r.c.w), pi, -1);
 }
 
 // A box group (rt_internal.h DevBox): slabs in the box frame give the entry and exit points of
@@ -541,14 +573,15 @@ RT_FN int box_field(int base, int code, int f, bool& present) {
 }
 // a face's key order, its primitive and whether the hit on it is valid (margin q >= 0, the face
 // exists, and it is not the face the ray leaves)
+template <bool kInst>
 RT_FN bool box_face(const RT_CAS DevBox* B, int f, real q, const RayCtx& R, int& ord, int& prim, bool with_prim) {
   bool present;
   ord = box_field(B->ord_base, B->ord_code, f, present);
   const int gid = box_field(B->gid_base, B->gid_code, f, present);
   if (with_prim) prim = box_field(B->prim_base, B->prim_code, f, present);
-  return present && gid != R.self_gid && q >= RL(0.0);
+  return present && !is_self<kInst>(R, gid, -1) && q >= RL(0.0);
 }
-template <bool kKeyOnly>
+template <bool kKeyOnly, bool kInst = false>
 RT_FN void test_box(const RT_CAS DevBox* B, const RayCtx& R, real tmin_up, Closest& C) {
   RT_COUNT(1);
   const f3 oc = R.o - f3{B->c[0], B->c[1], B->c[2]};
@@ -574,25 +607,29 @@ RT_FN void test_box(const RT_CAS DevBox* B, const RayCtx& R, real tmin_up, Close
   // the entry point is nearer than the exit point: the exit matters only when the entry is not
   // a valid hit (one key compare per box)
   int ord_n, ord_f, prim_n = 0, prim_f = 0;
-  const bool vn = box_face(B, fn, RMIN(gap, tn - tmin_up), R, ord_n, prim_n, !kKeyOnly);
-  const bool vf = box_face(B, ff, RMIN(gap, tf - tmin_up), R, ord_f, prim_f, !kKeyOnly);
-  consider<kKeyOnly>(C, vn ? tn : tf, (vn || vf) ? RL(0.0) : -RL(1.0), vn ? ord_n : ord_f, vn ? prim_n : prim_f);
+  const bool vn = box_face<kInst>(B, fn, RMIN(gap, tn - tmin_up), R, ord_n, prim_n, !kKeyOnly);
+  const bool vf = box_face<kInst>(B, ff, RMIN(gap, tf - tmin_up), R, ord_f, prim_f, !kKeyOnly);
+  consider<kKeyOnly, kInst>(C, vn ? tn : tf, (vn || vf) ? RL(0.0) : -RL(1.0), vn ? ord_n : ord_f,
+                            vn ? prim_n : prim_f, -1);
 }
 
 // BVH scenes: the surface set's large-primitive prefix (rt_build.cpp; P.flat_sets[0]), tested
 // before the traversal so that its closest hit bounds it.  The range is a kernel argument, so
 // the records are wave-uniform (scalar loads) even when only some lanes start a query here.
+template <bool kInst = false>
 RT_FN void prefix_hits(const KernelParams& P, cfp prims, const RayCtx& R, real tmin, Closest& C) {
   const DevFlatSet& S = P.flat_sets[0];
   if (!P.surface_prefix || (S.end == S.first && S.box_end == S.box_first)) return;
   const real tmin_up = float_up(tmin);
-  for (int b = S.box_first; b < S.box_end; ++b) test_box<false>((const RT_CAS DevBox*)P.boxes + b, R, tmin_up, C);
+  for (int b = S.box_first; b < S.box_end; ++b)
+    test_box<false, kInst>((const RT_CAS DevBox*)P.boxes + b, R, tmin_up, C);
   int k = S.first;
   const RT_CAS PrimRec64* rp = (const RT_CAS PrimRec64*)prims + k;
-  for (; k < S.end_quad; ++k, ++rp) test_static<RT_PRIM_CLASS_QUAD, false>(ld_rec64(rp), R, tmin, tmin_up, C, k);
-  for (; k < S.end_tri; ++k, ++rp) test_static<RT_PRIM_CLASS_TRI, false>(ld_rec64(rp), R, tmin, tmin_up, C, k);
+  for (; k < S.end_quad; ++k, ++rp)
+    test_static<RT_PRIM_CLASS_QUAD, false, kInst>(ld_rec64(rp), R, tmin, tmin_up, C, k);
+  for (; k < S.end_tri; ++k, ++rp) test_static<RT_PRIM_CLASS_TRI, false, kInst>(ld_rec64(rp), R, tmin, tmin_up, C, k);
   for (; k < S.end_sphere; ++k, ++rp)
-    test_static<RT_PRIM_CLASS_SPHERE, false>(ld_rec64(rp), R, tmin, tmin_up, C, k);
+    test_static<RT_PRIM_CLASS_SPHERE, false, kInst>(ld_rec64(rp), R, tmin, tmin_up, C, k);
 }
 
 
@@ -808,6 +845,8 @@ struct TravState {
   int node, leaf, sp;
   real tmin, tmin_up;
   Closest C;
+  int inst, ord_base;  // instancing: the placement being traversed (-1: world) and its key-order offset
+  f3 wo, wd;           // ... and the world ray, restored at RT_INST_EXIT
 };
 RT_FN void trav_begin(TravState& S, int root, real tmin) {
   S.node = root;
@@ -820,11 +859,18 @@ RT_FN void trav_begin(TravState& S, int root, real tmin) {
   S.tmin = tmin;
   S.tmin_up = float_up(tmin);
   S.C = no_hit();
+  S.inst = -1;
+  S.ord_base = 0;
 }
 RT_FN bool trav_done(const TravState& S) { return S.node == RT_EMPTY_ROOT && S.leaf == 0; }
 
 // One while-while round: descend until this lane (and the wave) holds a leaf, then test leaves.
-RT_FN void trav_round(const KernelParams& P, const RayCtx& R, TravState& S, const Trav& W, int& overflow) {
+// kInst (two-level instancing): a child RT_INST_FLAG | k enters placement k — the lane's ray R
+// is moved to object space, RT_INST_EXIT is pushed and the object's BVH is traversed; popping
+// RT_INST_EXIT restores the world ray.  t is the same in both spaces (rigid), so the closest
+// hit's bound carries over; a parked leaf is tested before the ray changes space.
+template <bool kInst = false, class RC>
+RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W, int& overflow) {
   constexpr int kDone = RT_EMPTY_ROOT;
   int* const stack = W.stack;
   const int stride = W.stride;
@@ -834,6 +880,45 @@ RT_FN void trav_round(const KernelParams& P, const RayCtx& R, TravState& S, cons
     return stack[S.sp * stride];
   };
   while (S.node >= 0) {
+    if constexpr (kInst) {
+      if (S.node >= RT_INST_FLAG) {
+        if (S.leaf != 0) break;  // test the parked leaf in the space it was found in
+        if (S.node == RT_INST_EXIT) {
+          R.o = S.wo;
+          R.d = S.wd;
+          prep_ray(R);
+          S.inst = -1;
+          S.ord_base = 0;
+          S.node = pop();
+          if (S.node < 0 && S.node != kDone) {  // a world leaf was the next entry: park it
+            S.leaf = S.node;
+            S.node = pop();
+          }
+        } else {
+          const int k = S.node - RT_INST_FLAG;
+          const RT_CAS DevInstance* I = inst_rec(P, k);
+          if (S.sp < P.stack_depth) {
+            stack[S.sp * stride] = RT_INST_EXIT;
+            ++S.sp;
+          } else {
+            overflow = 1;  // the stack is sized for world + object levels (rt_build.cpp): not reached
+          }
+          S.wo = R.o;
+          S.wd = R.d;
+          R.o = inst_to_object(I, R.o, true);
+          R.d = inst_to_object(I, R.d, false);
+          prep_ray(R);
+          S.inst = k;
+          S.ord_base = I->order;
+          S.node = I->root;
+          if (S.node < 0 && S.node != kDone) {  // the object is one leaf: park it, pop the exit
+            S.leaf = S.node;
+            S.node = pop();
+          }
+        }
+        continue;
+      }
+    }
     RT_COUNT(0);
     v4f n0, n1, n2;
     int cl, cr;
@@ -935,7 +1020,8 @@ RT_FN void trav_round(const KernelParams& P, const RayCtx& R, TravState& S, cons
     const int enc = ~S.leaf;
     const int first = enc >> RT_LEAF_SHIFT, count = (enc & ((1 << RT_LEAF_SHIFT) - 1)) + 1;
     for (int k = 0; k < count; ++k)
-      test_rec(P, ld_rec(cf(P.prims) + 16 * (size_t)(first + k)), first + k, R, S.tmin, S.tmin_up, S.C);
+      test_rec<false, kInst>(P, ld_rec(cf(P.prims) + 16 * (size_t)(first + k)), first + k, R, S.tmin, S.tmin_up, S.C,
+                             S.inst, S.ord_base);
 #ifdef RT_EXP_DOUBLE_LEAF  // ablation: every leaf tested twice (marginal cost of the leaf tests)
     for (int k = 0; k < count; ++k)
       test_rec(P, ld_rec(cf(P.prims) + 16 * (size_t)(first + k)), first + k, R, S.tmin,
@@ -1022,11 +1108,7 @@ RT_FN void camera_ray(const KernelParams& P, uint32_t pix, int sample, int px, i
   R.o = origin;
   R.d = normalize(target - origin);
   R.self_gid = -1;
-}
-
-RT_FN void prep_ray(RayCtx& R) {
-  R.idir = mk3(safe_rcp(R.d.x), safe_rcp(R.d.y), safe_rcp(R.d.z));
-  R.oidir = R.o * R.idir;
+  R.self_inst = -1;
 }
 
 // constantMedium's free-flight draw over the segment (lo, hi) (Geometry.hs:312-328); wm is the
@@ -1056,9 +1138,9 @@ RT_FN void medium_event(const KernelParams& P, int m, uint32_t pix, int sample, 
 // (and seg).  Returns true when the path terminates.
 // kMats: the scene has materials beyond lightSource / pitchBlack / lambertian; their code is
 // compiled only into those instantiations (the Cornell box and the bunny have none: -2.4 % / -1.2 %)
-template <int kTex, bool kMats>
+template <int kTex, bool kMats, bool kInst = false>
 RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int& seg, real tbest, int best,
-                 int hit_medium, RayCtx& R, f3& L, f3& T) {
+                 int hit_medium, RayCtx& R, f3& L, f3& T, int best_inst = -1) {
   RT_HOOK_SEGMENT(pix, sample, seg, R, tbest, best, hit_medium, L, T);
   if (hit_medium < 0 && best < 0) {
     // miss: cs_background (Ray.hs:179)
@@ -1075,6 +1157,12 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
   const RT_CAS DevMaterial* Mp = hit_medium >= 0
                                      ? (const RT_CAS DevMaterial*)P.mats + P.media[hit_medium].material
                                      : (const RT_CAS DevMaterial*)P.prim_shade + best;
+  if constexpr (kInst) {  // a placement's own material (the outermost `<$`) overrides its leaves'
+    if (hit_medium < 0 && best_inst >= 0) {
+      const int im = inst_rec(P, best_inst)->material;
+      if (im >= 0) Mp = (const RT_CAS DevMaterial*)P.mats + im;
+    }
+  }
   const DevMaterial Mt = DevMaterial{Mp->kind, Mp->tex, Mp->param, Mp->tex_const, {RL(0.), RL(0.), RL(0.)}, RL(0.)};
   // every material but pitchBlack and dielectric reads its texture; constant textures come with
   // the record, the others are evaluated once (one inlined copy keeps the register allocation down)
@@ -1090,7 +1178,21 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
     h.v = RL(0.);
     h.gid = -1;
   } else {
-    h = surface_info(P, prims, best, R, tbest, need_tex);
+    if constexpr (kInst) {
+      if (best_inst >= 0) {  // hit information in object space, point and normal back to world
+        const RT_CAS DevInstance* I = inst_rec(P, best_inst);
+        RayCtx Ro = R;
+        Ro.o = inst_to_object(I, R.o, true);
+        Ro.d = inst_to_object(I, R.d, false);
+        h = surface_info(P, prims, best, Ro, tbest, need_tex);
+        h.p = R.o + tbest * R.d;
+        h.n = inst_rotate(I, h.n);
+      } else {
+        h = surface_info(P, prims, best, R, tbest, need_tex);
+      }
+    } else {
+      h = surface_info(P, prims, best, R, tbest, need_tex);
+    }
   }
   f3 tex = f3{Mp->c0[0], Mp->c0[1], Mp->c0[2]};
   if (need_tex) tex = eval_texture<kTex == 2>(P, Mt.tex, h.u, h.v, h.p);
@@ -1196,6 +1298,7 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
       R.o = h.p;
       R.d = newdir;
       R.self_gid = h.gid;
+      if constexpr (kInst) R.self_inst = hit_medium >= 0 ? -1 : best_inst;
       ++seg;
     }
   }
@@ -1251,6 +1354,7 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
   R.o = R.d = R.idir = R.oidir = L;
   R.time = RL(0.0);
   R.self_gid = -1;
+  R.self_inst = -1;
   for (;;) {
     const bool need = !alive && I.sample >= I.s_end;
     if (need && I.item >= 0) commit(I.tp, acc, bad);
@@ -1325,7 +1429,7 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
 // entering it, the second (Geometry.hs:306-328) — each starting inside the traversal loop as
 // soon as the previous one finishes.
 enum : int { ST_NEED_ITEM = 0, ST_NEED_SAMPLE = 1, ST_START_SEG = 2, ST_TRACE = 3, ST_SHADE = 4 };
-template <int kTex, bool kMedia, bool kMats, class Grab, class Commit>
+template <int kTex, bool kMedia, bool kMats, bool kInst, class Grab, class Commit>
 RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW, const real* prims_) {
   const cfp prims = cf(prims_);
   const int n_media = kMedia ? P.n_media : 0;  // media code only in the kMedia instantiations
@@ -1341,10 +1445,11 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
   R.o = R.d = R.idir = R.oidir = L;
   R.time = RL(0.0);
   R.self_gid = -1;
+  R.self_inst = -1;
   TravState S;
   trav_begin(S, RT_EMPTY_ROOT, kTmin);
   // query sequencing within a segment: q = 0 surfaces; q = 1 + 2m / 2 + 2m medium m, 1st / 2nd hit
-  int q = 0, best = -1, hit_medium = -1;
+  int q = 0, best = -1, hit_medium = -1, best_inst = -1;
   real tbest = kInf, t1 = RL(0.0), t_surf = kInf;
   for (;;) {
     // ---- front end: items, samples, segment starts (lanes not tracing)
@@ -1369,10 +1474,11 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
       prep_ray(R);
       q = 0;
       best = -1;
+      best_inst = -1;
       hit_medium = -1;
       tbest = kInf;
       trav_begin(S, P.surface_root, kTmin);
-      prefix_hits(P, prims, R, kTmin, S.C);
+      prefix_hits<kInst>(P, prims, R, kTmin, S.C);
       state = ST_TRACE;
     }
     // ---- traversal rounds; a finished query starts the segment's next one in place
@@ -1383,12 +1489,13 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
       const int n_live = RT_BALLOT_COUNT(true);
       if (n_tr < n_live && n_tr * 100 <= n_live * P.trav_exit_pct) break;
       if (tr) {
-        trav_round(P, R, S, TW, overflow);
+        trav_round<kInst>(P, R, S, TW, overflow);
         while (trav_done(S)) {
           int next_m = -1;  // medium whose first query starts next
           if (q == 0) {
             tbest = t_surf = S.C.t;
             best = S.C.prim;
+            best_inst = S.C.inst;
             next_m = 0;
           } else {
             const int m = (q - 1) >> 1;
@@ -1426,13 +1533,13 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
           }
           // a query over a set that is a single leaf (e.g. a fog sphere) is tested right away
           if (state != ST_TRACE || S.node != RT_EMPTY_ROOT) break;
-          trav_round(P, R, S, TW, overflow);
+          trav_round<kInst>(P, R, S, TW, overflow);
         }
       }
     }
     // ---- shade the segments whose queries are complete
     if (state == ST_SHADE) {
-      if (shade<kTex, kMats>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T)) {
+      if (shade<kTex, kMats, kInst>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T, best_inst)) {
         RT_HOOK_SAMPLE(I.pix, I.sample, L);
         acc_sample(acc, L, bad);
         ++I.sample;

@@ -160,6 +160,36 @@ def _pawn_world(mesh, fog):
     return group(objs)
 
 
+def bunny_instances(width=400, spp=64, depth=50, n=3):
+    """Two-level instancing test scene (not a reference scene): the Cornell walls and light
+    around an n x n grid of the SAME bunny mesh object (object space: centred)
+    placed by rigid transforms (rotateY by a different angle, translate), with materials applied
+    outside the transforms (lambertian colours, one mirror, one dielectric) — every placement is
+    an rt_instance of one object (Geometry.hs:382-391).  The object is scaled 900 * 3 / n so the
+    grid fits the room for any n."""
+    mesh = load_mesh("bunny.obj")
+    center = tuple(midpoint(i) for i in boundingBox(triangleMesh(mesh)))
+    obj_mesh = transformVertices(scale(900 * 3 / max(n, 3)) @ translate(tuple(-c for c in center)), mesh)
+    ymin = min(v[1] for v in obj_mesh.vertices)
+    bunny = triangleMesh(obj_mesh)  # one object, shared by every placement below
+    walls, white = cornell_walls()
+    placed = []
+    for i in range(n):
+        for j in range(n):
+            k = i * n + j
+            x, z = 100 + 355 * (i + 0.5) / n, 100 + 355 * (j + 0.5) / n
+            m = translate(V3(x, -ymin, z)) @ rotateY(degrees(40 * k))
+            if k == 1:
+                mat = mirror(constantTexture(V3(0.9, 0.9, 0.9)))
+            elif k == n * n - 1:
+                mat = dielectric(1.5)
+            else:
+                mat = lambertian(constantTexture(V3(0.3 + 0.07 * (k % 10), 0.5, 0.8 - 0.06 * (k % 10))))
+            placed.append(mat << transform(m, bunny))
+    world = group(walls + placed)
+    return cornell_settings(width, spp, depth, redirect=True), world, mkStdGen(91)
+
+
 def pawn_test(width=500, spp=400, depth=20):
     mesh = transformVertices(scale(100), load_mesh("pawn.obj"))
     settings = defaultCameraSettings(cs_center=V3(0, 3.75, 5), cs_lookAt=V3(0, 2.75, 0), cs_imageWidth=width,
@@ -219,4 +249,5 @@ CONFIGS = {
     "pawn_test": pawn_test,
     "noise_test": noise_test,
     "box_gallery": box_gallery,
+    "bunny_instances": bunny_instances,
 }

@@ -28,16 +28,17 @@ struct Commit {
 };
 
 template <int kTex, bool kMedia, bool kMats, class G, class Cm>
-int run_loop(const RT_NS::KernelParams& P, int base, G& g, Cm& c, const RT_NS::Trav& W) {
-  switch (base) {
+int run_loop(const RT_NS::KernelParams& P, int variant, G& g, Cm& c, const RT_NS::Trav& W) {
+  if (variant & RT_VAR_INST) return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, true>(P, g, c, W, P.prims);
+  switch (variant & RT_VAR_BASE) {
     case RT_VAR_FLAT: return RT_NS::lane_loop_lockstep<true, kTex, kMedia, kMats>(P, g, c, W, P.prims);
     case RT_VAR_BVH_LOCKSTEP: return RT_NS::lane_loop_lockstep<false, kTex, kMedia, kMats>(P, g, c, W, P.prims);
-    default: return RT_NS::lane_loop_bvh<kTex, kMedia, kMats>(P, g, c, W, P.prims);
+    default: return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, false>(P, g, c, W, P.prims);
   }
 }
 template <int kTex, class G, class Cm>
 int run_flags(const RT_NS::KernelParams& P, int variant, G& g, Cm& c, const RT_NS::Trav& W) {
-  const int base = variant & RT_VAR_BASE;
+  const int base = variant;
   const bool media = (variant & RT_VAR_MEDIA) != 0, mats = (variant & RT_VAR_MATS) != 0;
   if (media) return mats ? run_loop<kTex, true, true>(P, base, g, c, W) : run_loop<kTex, true, false>(P, base, g, c, W);
   return mats ? run_loop<kTex, false, true>(P, base, g, c, W) : run_loop<kTex, false, false>(P, base, g, c, W);
@@ -83,6 +84,7 @@ int render(const HostScene& H, const rt_camera_settings* cs, uint64_t seed, cons
   P.perlin_grad = A.perlin_grad.data();
   P.flat_recs = A.flat_recs.data();
   P.boxes = A.boxes.data();
+  P.instances = A.instances.data();
   P.out = out;
   P.surface_root = H.surface_root;
   P.leaf_exit_pct = H.leaf_exit_pct;
@@ -107,7 +109,7 @@ int render(const HostScene& H, const rt_camera_settings* cs, uint64_t seed, cons
   for (auto& f : flags) f = 0;
   Shared s;
   s.P = &P;
-  s.variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex);
+  s.variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex, H.n_instances > 0);
   s.accum = &accum;
   s.flags = &flags;
   for (auto& c : s.cnt) c = 0;

@@ -373,6 +373,24 @@ def test_moving_and_transform_against_oracle(gpu, oracle_mod, precision):
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("n", [3, 8])
+def test_two_level_instancing_against_oracle(gpu, oracle_mod, n, precision):
+    """n x n rigid placements of ONE bunny object traced as rt_instances (world BVH over instance
+    boxes -> object-space BLAS, ray moved by the inverse 3x4) against the oracle's walk of the
+    reference's `transform` (Geometry.hs:382-391), and against the transforms baked into world
+    triangles (instance_min=0)."""
+    from raytrace_amd import scene as S
+    cs, world, seed = scenes.bunny_instances(width=96, spp=8, n=n)
+    inst = S.flatten(world)
+    assert len(inst.instances) == n * n
+    ref = oracle_mod.render(cs, world, seed, mode=oracle_mod.RNG_PHILOX)
+    img = R.raytrace(cs, inst, seed, precision=precision)
+    assert_parity(img, ref, precision, 0.99, _floor()["cornell"], f"instances{n}", 8, 15.0)
+    baked = R.raytrace(cs, S.flatten(world, instance_min=0), seed, precision=precision)
+    assert_parity(baked, ref, precision, 0.99, _floor()["cornell"], f"baked{n}", 8, 15.0)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
 def test_device_scene_async_and_encode8_bit_exact(gpu, precision):
     torch = gpu
     from raytrace_amd import _lib

@@ -195,6 +195,31 @@ def test_box_groups_match_per_face_tests(oracle_mod, emu_mod, monkeypatch, name)
     np.testing.assert_allclose(a.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=5e-3)
 
 
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("n", [1, 3, 8])
+def test_two_level_instancing_matches_oracle(oracle_mod, emu_mod, n, precision):
+    """n x n placements of ONE bunny object (rt_instance, 2-level BVH: world boxes -> object-space
+    BLAS) against the oracle, which walks the reference's `transform` (ray into object space,
+    Geometry.hs:382-391) on the same Philox numbers, and against the same scene with the
+    transforms baked into world-space triangles (instance_min=0)."""
+    from raytrace_amd import scene as S
+    cs, world, seed = scenes.bunny_instances(width=48, spp=4, n=n)
+    inst = S.flatten(world)
+    baked = S.flatten(world, instance_min=0)
+    assert len(inst.instances) == n * n and len(baked.instances) == 0
+    assert len(inst.prims) < len(baked.prims) or n == 1
+    ref = oracle_mod.render(cs, world, seed, mode=oracle_mod.RNG_PHILOX)
+    for flat in (inst, baked):
+        got = emu_mod.render(cs, flat, seed, precision=precision)
+        assert np.isfinite(got).all()
+        if precision == "f64":
+            rel = (np.abs(got - ref) / np.maximum(np.abs(ref), 1e-3)).max(-1)
+            assert (rel <= 1e-9).mean() >= 0.999
+        else:
+            assert pixel_agreement(got, ref) >= 0.99
+        np.testing.assert_allclose(got.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=5e-3)
+
+
 def test_perlin_tables(oracle_mod):
     """The product's Perlin tables: three permutations of 0..255 (Noise.hs:60-92) and the 256
     gradients of Noise.hs:94-98, identical to the oracle's independent C restatement."""
