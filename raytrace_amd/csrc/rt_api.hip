@@ -419,4 +419,11 @@ int rt_encode8_async(const void* d_rgb, int32_t in_f64, uint8_t* d_out, int64_t 
   return RT_OK;
 }
 
+#if defined(RT_PHASE_PROF)
+// diagnostic build only: the BVH kernel's phase counters (rt_trace.h RT_PHASE_PROF), read and zeroed
+int rt_prof_read(int f64, unsigned long long* out, int n) {
+  return f64 ? rt_prof_read_kernel((const KernelParams64*)nullptr, out, n) : rt_prof_read_kernel((const KernelParams*)nullptr, out, n);
+}
+#endif
+
 }  // extern "C"

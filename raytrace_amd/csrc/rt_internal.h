@@ -332,6 +332,10 @@ int rt_launch_render(const KernelParams64& p, int grid_blocks, int variant, void
 // accum / nanflag -> out (mean over spp, NaN where flagged)
 int rt_launch_resolve(const KernelParams& p, void* stream);
 int rt_launch_resolve(const KernelParams64& p, void* stream);
+#if defined(RT_PHASE_PROF)
+int rt_prof_read_kernel(const KernelParams*, unsigned long long* out, int n);
+int rt_prof_read_kernel(const KernelParams64*, unsigned long long* out, int n);
+#endif
 // 8-bit epilogue over float (in_f64 = 0) or binary64 (1) values; thr: 256 host thresholds
 int rt_launch_encode8(const void* in, int in_f64, uint8_t* out, int64_t n, const double* thr, int encoding,
                       void* stream);

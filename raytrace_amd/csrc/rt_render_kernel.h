@@ -279,6 +279,18 @@ int rt_launch_render(const KernelParamsT<RT_NS::real>& p, int grid_blocks, int v
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+#if defined(RT_PHASE_PROF)
+// diagnostic build: read (and zero) the phase counters of this precision's BVH kernel
+int rt_prof_read_kernel(const KernelParamsT<RT_NS::real>*, unsigned long long* out, int n) {
+  using namespace RT_NS;
+  if (n > PF_N) n = PF_N;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rt_prof_buf), n * sizeof(unsigned long long)) != hipSuccess) return -1;
+  unsigned long long zero[PF_N] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(rt_prof_buf), zero, sizeof(zero)) == hipSuccess ? n : -1;
+}
+#endif
+
 int rt_launch_resolve(const KernelParamsT<RT_NS::real>& p, void* stream) {
   using namespace RT_NS;
   int n = p.tile_rows * p.cam.width;

@@ -838,6 +838,36 @@ RT_FN void acc_sample(Acc& A, f3 L, bool& bad) {
   acc_add(A, 2, L.z, bad);
 }
 
+// Diagnostic build only (make exp DEFS=-DRT_PHASE_PROF, tools/phase_prof.py): per-wave shader
+// clocks and lane counts by phase of lane_loop_bvh and trav_round, summed over the launch into
+// rt_prof_buf.
+#if defined(RT_PHASE_PROF) && !defined(RT_HOST_EMU)
+enum : int { PF_FRONT, PF_TRAV, PF_SHADE, PF_ITERS, PF_ROUNDS, PF_TRACING, PF_LIVE, PF_SHADING, PF_FRONT_LANES,
+             PF_NODE_STEPS, PF_NODE_LANES, PF_LEAF_STEPS, PF_LEAF_LANES, PF_NODE_CLK, PF_LEAF_CLK, PF_N };
+__device__ unsigned long long rt_prof_buf[PF_N];
+#define RT_PROF_DECL unsigned long long prof[PF_N] = {}; unsigned long long pf_t0 = clock64(), pf_t1;
+#define RT_PROF_MARK(k) (pf_t1 = clock64(), prof[k] += pf_t1 - pf_t0, pf_t0 = pf_t1)
+#define RT_PROF_ADD(k, x) (prof[k] += (unsigned long long)(x))
+#define RT_PROF_FLUSH                                                       \
+  if ((threadIdx.x & 63) == 0)                                              \
+    for (int k = 0; k < PF_N; ++k) atomicAdd(&rt_prof_buf[k], prof[k]);
+#define RT_PROF_PARAM , unsigned long long* prof
+#define RT_PROF_ARG , prof
+#define RT_PROF_NULLARG , (unsigned long long*)nullptr
+#define RT_PROF_PADD(k, x) (prof ? (void)(prof[k] += (unsigned long long)(x)) : (void)0)
+#define RT_PROF_CLK() clock64()
+#else
+#define RT_PROF_DECL
+#define RT_PROF_MARK(k) ((void)0)
+#define RT_PROF_ADD(k, x) ((void)0)
+#define RT_PROF_FLUSH
+#define RT_PROF_PARAM
+#define RT_PROF_ARG
+#define RT_PROF_NULLARG
+#define RT_PROF_PADD(k, x) ((void)0)
+#define RT_PROF_CLK() 0ull
+#endif
+
 // ---------------------------------------------------------------- BVH traversal
 // Resumable per-lane BVH traversal (the body of trace_set, split so a lane can stop between
 // rounds and continue in a later iteration of the lane loop with its state intact).
@@ -870,7 +900,8 @@ RT_FN bool trav_done(const TravState& S) { return S.node == RT_EMPTY_ROOT && S.l
 // RT_INST_EXIT restores the world ray.  t is the same in both spaces (rigid), so the closest
 // hit's bound carries over; a parked leaf is tested before the ray changes space.
 template <bool kInst = false, class RC>
-RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W, int& overflow) {
+RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W, int& overflow RT_PROF_PARAM) {
+  unsigned long long pf_c0 = RT_PROF_CLK();
   constexpr int kDone = RT_EMPTY_ROOT;
   int* const stack = W.stack;
   const int stride = W.stride;
@@ -880,6 +911,8 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
     return stack[S.sp * stride];
   };
   while (S.node >= 0) {
+    RT_PROF_PADD(PF_NODE_STEPS, 1);
+    RT_PROF_PADD(PF_NODE_LANES, RT_BALLOT_COUNT(true));
     if constexpr (kInst) {
       if (S.node >= RT_INST_FLAG) {
         if (S.leaf != 0) break;  // test the parked leaf in the space it was found in
@@ -1016,7 +1049,11 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
     // Aila & Laine's while-while); the rest keep their state and descend in the next round
     if (RT_BALLOT_COUNT(S.leaf != 0) * 100 >= RT_BALLOT_COUNT(true) * P.leaf_exit_pct) break;
   }
+  unsigned long long pf_c1 = RT_PROF_CLK();
+  RT_PROF_PADD(PF_NODE_CLK, pf_c1 - pf_c0);
   while (S.leaf < 0) {
+    RT_PROF_PADD(PF_LEAF_STEPS, 1);
+    RT_PROF_PADD(PF_LEAF_LANES, RT_BALLOT_COUNT(true));
     const int enc = ~S.leaf;
     const int first = enc >> RT_LEAF_SHIFT, count = (enc & ((1 << RT_LEAF_SHIFT) - 1)) + 1;
     for (int k = 0; k < count; ++k)
@@ -1033,6 +1070,9 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
       S.node = pop();
     }
   }
+  RT_PROF_PADD(PF_LEAF_CLK, RT_PROF_CLK() - pf_c1);
+  (void)pf_c0;
+  (void)pf_c1;
 }
 
 // kFlat: the set is one flat leaf (rt_internal.h DevFlatSet); every lane walks the same
@@ -1082,7 +1122,7 @@ RT_FN_SPEC void closest<false>(const KernelParams& P, cfp prims, int root, int s
   TravState S;
   trav_begin(S, root, tmin);
   if (set == 0) prefix_hits(P, prims, R, tmin, S.C);
-  while (!trav_done(S)) trav_round(P, R, S, W, *overflow);
+  while (!trav_done(S)) trav_round(P, R, S, W, *overflow RT_PROF_NULLARG);
   C = S.C;
 }
 
@@ -1451,9 +1491,12 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
   // query sequencing within a segment: q = 0 surfaces; q = 1 + 2m / 2 + 2m medium m, 1st / 2nd hit
   int q = 0, best = -1, hit_medium = -1, best_inst = -1;
   real tbest = kInf, t1 = RL(0.0), t_surf = kInf;
+  RT_PROF_DECL
   for (;;) {
     // ---- front end: items, samples, segment starts (lanes not tracing)
     const bool need = state == ST_NEED_ITEM;
+    RT_PROF_ADD(PF_ITERS, 1);
+    RT_PROF_ADD(PF_FRONT_LANES, RT_BALLOT_COUNT(state != ST_TRACE));
     if (need && I.item >= 0) commit(I.tp, acc, bad);
     const int got = grab(need);
     if (need) {
@@ -1481,6 +1524,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
       prefix_hits<kInst>(P, prims, R, kTmin, S.C);
       state = ST_TRACE;
     }
+    RT_PROF_MARK(PF_FRONT);
     // ---- traversal rounds; a finished query starts the segment's next one in place
     for (;;) {
       const bool tr = state == ST_TRACE;
@@ -1488,8 +1532,11 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
       if (n_tr == 0) break;
       const int n_live = RT_BALLOT_COUNT(true);
       if (n_tr < n_live && n_tr * 100 <= n_live * P.trav_exit_pct) break;
+      RT_PROF_ADD(PF_ROUNDS, 1);
+      RT_PROF_ADD(PF_TRACING, n_tr);
+      RT_PROF_ADD(PF_LIVE, n_live);
       if (tr) {
-        trav_round<kInst>(P, R, S, TW, overflow);
+        trav_round<kInst>(P, R, S, TW, overflow RT_PROF_ARG);
         while (trav_done(S)) {
           int next_m = -1;  // medium whose first query starts next
           if (q == 0) {
@@ -1533,10 +1580,12 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
           }
           // a query over a set that is a single leaf (e.g. a fog sphere) is tested right away
           if (state != ST_TRACE || S.node != RT_EMPTY_ROOT) break;
-          trav_round<kInst>(P, R, S, TW, overflow);
+          trav_round<kInst>(P, R, S, TW, overflow RT_PROF_ARG);
         }
       }
     }
+    RT_PROF_MARK(PF_TRAV);
+    RT_PROF_ADD(PF_SHADING, RT_BALLOT_COUNT(state == ST_SHADE));
     // ---- shade the segments whose queries are complete
     if (state == ST_SHADE) {
       if (shade<kTex, kMats, kInst>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T, best_inst)) {
@@ -1548,7 +1597,9 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
         state = ST_START_SEG;
       }
     }
+    RT_PROF_MARK(PF_SHADE);
   }
+  RT_PROF_FLUSH
   return overflow;
 }
 
