@@ -966,14 +966,32 @@ void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes) {
     int c = std::atoi(env);
     if (c > 0) chunk = c;
   }
-  const int n_chunks = (spp + chunk - 1) / chunk;
-  long long items = (long long)n_chunks * tile_pixels;
-  if (items > 0x7fffff00LL) {  // keep item ids in int: grow the chunk
+  // Big items for the bulk of the samples, small ones for the tail: the first samples of every
+  // pixel go in 16-sample items (a quarter of the commit atomics, 7 % of the binary64 Cornell
+  // kernel), the last T in `chunk`-sample items, T such that the tail alone still gives every
+  // resident lane RT_TAIL_ITEMS_* items (the queue's end stays as short as with small items only).
+  int big = 16, n_big = 0;
+  if (const char* env = std::getenv("RT_AMD_BIG_CHUNK")) big = std::max(1, std::atoi(env));
+  int tail_items = sizeof(R) == 8 ? RT_TAIL_ITEMS_F64 : RT_TAIL_ITEMS_F32;
+  if (const char* env = std::getenv("RT_AMD_TAIL_ITEMS")) tail_items = std::atoi(env);
+  if (chunk < big && tail_items > 0 && resident_lanes > 0 && tile_pixels > 0) {
+    long long t = ((long long)tail_items * chunk * resident_lanes + tile_pixels - 1) / tile_pixels;
+    if (const char* env = std::getenv("RT_AMD_TAIL_SAMPLES")) t = std::max(0, std::atoi(env));  // tests
+    const long long tail = ((t + chunk - 1) / chunk) * chunk;  // tail samples, a multiple of chunk
+    if (tail < spp) n_big = (int)((spp - tail) / big);
+  }
+  const int n_chunks = (spp - n_big * big + chunk - 1) / chunk;
+  long long items = (long long)(n_big + n_chunks) * tile_pixels;
+  if (items > 0x7fffff00LL) {  // keep item ids in int: one item size, grow the chunk
+    n_big = 0;
     chunk = (int)((long long)spp * tile_pixels / 0x7fffff00LL) + 1;
     items = (long long)((spp + chunk - 1) / chunk) * tile_pixels;
   }
   P.chunk = chunk;
-  P.n_chunks = (spp + chunk - 1) / chunk;
+  P.n_chunks = (spp - n_big * big + chunk - 1) / chunk;
+  P.big_chunk = big;
+  P.n_big_chunks = n_big;
+  P.n_big_items = (int)((long long)n_big * tile_pixels);
   P.n_items = (int)items;
 }
 

@@ -34,6 +34,15 @@
 #define RT_MAX_TARGETS 8
 #ifndef RT_LEAF_MAX
 #define RT_LEAF_MAX 8
+// small items per resident lane kept for the queue tail (rt_build.cpp rt_host_plan_work; 0: one
+// item size).  Cornell 600x600x200, same box (profiles/r2/items/): binary64 6.77 -> 6.63 ms at
+// 16 (8: 6.69, 32: 6.64, 64: 6.78); FP32 3.50 -> 3.46 at 32 (16: 3.49); 8-GPU shares unchanged
+#ifndef RT_TAIL_ITEMS_F64
+#define RT_TAIL_ITEMS_F64 16
+#endif
+#ifndef RT_TAIL_ITEMS_F32
+#define RT_TAIL_ITEMS_F32 32
+#endif
 #endif
 #define RT_LEAF_SHIFT 6       // leaf encoding ~(first << 6 | count - 1), count <= 64
 #define RT_FLAT_MAX 32        // a set of at most this many leaves is one flat leaf (no traversal)
@@ -228,9 +237,15 @@ struct KernelParamsT {
   unsigned long long* accum;  // fixed-point radiance sums per tile pixel: RT_ACC_WORDS(R) x int64
   unsigned int* nanflag;      // per tile pixel: a sample produced a non-finite radiance
   int* counter;               // next unclaimed item
-  int chunk;                  // samples per item
-  int n_chunks;
-  int n_items;
+  // two item sizes: the first n_big_items = n_big_chunks x tile pixels items cover samples
+  // [0, n_big_chunks * big_chunk) of their pixel in big_chunk-sample chunks (fewer commits), the
+  // rest cover the remaining samples in chunk-sample chunks (a short queue tail)
+  int chunk;                  // samples per (small) item
+  int n_chunks;               // small chunks per pixel
+  int n_items;                // all items
+  int big_chunk;              // samples per big item
+  int n_big_chunks;           // big chunks per pixel (0: one item size)
+  int n_big_items;
   int stack_depth;            // LDS stack entries per lane (>= the scene's BVH depth)
   int lds_nodes;              // BVH nodes [0, lds_nodes) are read from the workgroup's LDS copy
   int trav_exit_pct;          // BVH kernel: leave traversal when <= this % of live lanes trace

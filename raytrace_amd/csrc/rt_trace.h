@@ -1358,17 +1358,21 @@ RT_FN uint32_t fast_div(uint32_t n, const FastDiv& f) {
 RT_FN bool open_item(const KernelParams& P, int item, ItemCtx& I) {
   const int W = P.cam.width, tile_pixels = P.tile_rows * W;
   I.item = item;
+  // big items first (samples [0, n_big_chunks * big_chunk) of each pixel), then the small ones
+  const bool big = item < P.n_big_items;
+  const int id = big ? item : item - P.n_big_items;
   // item, tile pixel and row are non-negative: exact multiply-shift division by the launch
   // constants instead of the ~20-instruction signed integer division sequences
-  const int k = (int)fast_div((uint32_t)item, P.div_tile);
-  I.tp = item - k * tile_pixels;
+  const int k = (int)fast_div((uint32_t)id, P.div_tile);
+  I.tp = id - k * tile_pixels;
   const int tr = (int)fast_div((uint32_t)I.tp, P.div_width);
   I.px = I.tp - tr * W;
   const int tb = (int)fast_div((uint32_t)tr, P.div_block);
   I.gy = (tb * P.n_shards + P.shard) * P.row_block + (tr - tb * P.row_block);
   I.pix = (uint32_t)(I.gy * W + I.px);
-  I.sample = k * P.chunk;
-  I.s_end = I.sample + P.chunk < P.cam.spp ? I.sample + P.chunk : P.cam.spp;
+  const int chunk = big ? P.big_chunk : P.chunk;
+  I.sample = (big ? 0 : P.n_big_chunks * P.big_chunk) + k * chunk;
+  I.s_end = I.sample + chunk < P.cam.spp ? I.sample + chunk : P.cam.spp;
   if (I.gy >= P.cam.height || P.cam.max_depth <= 0) I.s_end = I.sample;  // padding row / black image
   return I.sample < I.s_end;
 }

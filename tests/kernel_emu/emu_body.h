@@ -99,6 +99,8 @@ int render(const HostScene& H, const rt_camera_settings* cs, uint64_t seed, cons
   if (chunk > 0) {
     P.chunk = chunk;
     P.n_chunks = (P.cam.spp + chunk - 1) / chunk;
+    P.n_big_chunks = 0;
+    P.n_big_items = 0;
     P.n_items = P.n_chunks * P.tile_rows * P.cam.width;
   }
   const size_t tile_pixels = (size_t)P.tile_rows * P.cam.width;

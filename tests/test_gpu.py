@@ -228,14 +228,19 @@ def test_box_groups_match_oracle(gpu, oracle_mod, monkeypatch, name, precision):
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("name", ["cornell", "bunny_cornell"])
 def test_item_chunk_does_not_change_the_image(gpu, monkeypatch, name, precision):
-    """Items of 1, 3 (ragged: does not divide spp), 4 and 16 samples: a different work split
-    and commit order, the same fixed-point sums — bit-identical images."""
+    """Items of 1, 3 (ragged: does not divide spp), 4 and 16 samples, and two item sizes: a
+    different work split and commit order, the same fixed-point sums — bit-identical images."""
     fn = {"cornell": scenes.cornell_box, "bunny_cornell": scenes.bunny_cornell}[name]
     cs, world, seed = fn(width=64, spp=20)
     imgs = []
     for c in ("1", "3", "4", "16"):
         monkeypatch.setenv("RT_AMD_CHUNK", c)
         imgs.append(R.raytrace(cs, world, seed, precision=precision))
+    # two item sizes (big items of 7 samples first, a tail of 3-sample items)
+    monkeypatch.setenv("RT_AMD_CHUNK", "3")
+    monkeypatch.setenv("RT_AMD_BIG_CHUNK", "7")
+    monkeypatch.setenv("RT_AMD_TAIL_SAMPLES", "6")
+    imgs.append(R.raytrace(cs, world, seed, precision=precision))
     for img in imgs[1:]:
         assert np.array_equal(img, imgs[0], equal_nan=True)
 
