@@ -146,7 +146,7 @@ int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_
   P.stack_depth = s->stack_depth;
   P.lds_nodes = s->lds_nodes;
   P.n_prims = s->n_prims;
-  rt_host_plan_work(P, (long long)A.resident_blocks * rt_block_of(s->variant));
+  rt_host_plan_work(P, (long long)A.resident_blocks * rt_block_of(s->variant), (s->variant & RT_VAR_BASE) == RT_VAR_FLAT);
   P.trav_exit_pct = s->trav_exit_pct;
   HIP_TRY(hipSetDevice(s->device));
   // stream-ordered workspace: fixed-point sums, NaN flags, queue counter (graph-capturable)

@@ -944,7 +944,7 @@ FastDiv rt_host_fastdiv(uint32_t d) {
 }
 
 template <class R>
-void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes) {
+void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_sizes) {
   P.div_tile = rt_host_fastdiv((uint32_t)P.tile_rows * (uint32_t)P.cam.width);
   P.div_width = rt_host_fastdiv((uint32_t)P.cam.width);
   P.div_block = rt_host_fastdiv((uint32_t)P.row_block);
@@ -974,7 +974,7 @@ void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes) {
   if (const char* env = std::getenv("RT_AMD_BIG_CHUNK")) big = std::max(1, std::atoi(env));
   int tail_items = sizeof(R) == 8 ? RT_TAIL_ITEMS_F64 : RT_TAIL_ITEMS_F32;
   if (const char* env = std::getenv("RT_AMD_TAIL_ITEMS")) tail_items = std::atoi(env);
-  if (chunk < big && tail_items > 0 && resident_lanes > 0 && tile_pixels > 0) {
+  if (two_sizes && chunk < big && tail_items > 0 && resident_lanes > 0 && tile_pixels > 0) {
     long long t = ((long long)tail_items * chunk * resident_lanes + tile_pixels - 1) / tile_pixels;
     if (const char* env = std::getenv("RT_AMD_TAIL_SAMPLES")) t = std::max(0, std::atoi(env));  // tests
     const long long tail = ((t + chunk - 1) / chunk) * chunk;  // tail samples, a multiple of chunk
@@ -991,7 +991,7 @@ void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes) {
   P.n_chunks = (spp - n_big * big + chunk - 1) / chunk;
   P.big_chunk = big;
   P.n_big_chunks = n_big;
-  P.n_big_items = (int)((long long)n_big * tile_pixels);
+  P.small_base = n_big * (big - chunk);
   P.n_items = (int)items;
 }
 
@@ -999,8 +999,8 @@ template int rt_host_make_params<float>(const rt_camera_settings*, uint64_t, con
                                         std::string&);
 template int rt_host_make_params<double>(const rt_camera_settings*, uint64_t, const rt_exec*, KernelParamsT<double>&,
                                          std::string&);
-template void rt_host_plan_work<float>(KernelParamsT<float>&, long long);
-template void rt_host_plan_work<double>(KernelParamsT<double>&, long long);
+template void rt_host_plan_work<float>(KernelParamsT<float>&, long long, bool);
+template void rt_host_plan_work<double>(KernelParamsT<double>&, long long, bool);
 
 // The 8-bit code thresholds of writeImage / writeImageSqrt's quantisation (rt_encode8_table.h,
 // generated with the transfer evaluated exactly; raytrace_amd.ray.encode8 reads the same table).

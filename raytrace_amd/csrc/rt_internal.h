@@ -237,15 +237,16 @@ struct KernelParamsT {
   unsigned long long* accum;  // fixed-point radiance sums per tile pixel: RT_ACC_WORDS(R) x int64
   unsigned int* nanflag;      // per tile pixel: a sample produced a non-finite radiance
   int* counter;               // next unclaimed item
-  // two item sizes: the first n_big_items = n_big_chunks x tile pixels items cover samples
+  // two item sizes: the first n_big_chunks x tile pixels items cover samples
   // [0, n_big_chunks * big_chunk) of their pixel in big_chunk-sample chunks (fewer commits), the
   // rest cover the remaining samples in chunk-sample chunks (a short queue tail)
   int chunk;                  // samples per (small) item
   int n_chunks;               // small chunks per pixel
   int n_items;                // all items
   int big_chunk;              // samples per big item
-  int n_big_chunks;           // big chunks per pixel (0: one item size)
-  int n_big_items;
+  int n_big_chunks;           // big chunks per pixel (0: one item size); big items are the first
+                              // n_big_chunks x tile pixels ids
+  int small_base;             // n_big_chunks x (big_chunk - chunk): small chunk k starts at small_base + k chunk
   int stack_depth;            // LDS stack entries per lane (>= the scene's BVH depth)
   int lds_nodes;              // BVH nodes [0, lds_nodes) are read from the workgroup's LDS copy
   int trav_exit_pct;          // BVH kernel: leave traversal when <= this % of live lanes trace
@@ -332,7 +333,7 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
                         std::string& err);
 // work decomposition (rt_build.cpp): chunk so that items >= ~8 x resident lanes
 template <class R>
-void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes);
+void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_sizes);  // two_sizes: flat kernel
 FastDiv rt_host_fastdiv(uint32_t d);
 // the 8-bit code thresholds of the output epilogue (rt_build.cpp): thr[k] = the smallest binary64
 // x in [0, 1] whose code min(255, floor(256 transfer(x))) is >= k (k = 1..255; thr[0] = 0)

@@ -1355,23 +1355,26 @@ RT_FN uint32_t fast_div(uint32_t n, const FastDiv& f) {
   const uint32_t t = (uint32_t)(((uint64_t)n * f.m) >> 32);
   return (t + ((n - t) >> 1)) >> f.s;
 }
+// kTwoSizes: the item may be big (flat kernel only: the BVH kernels run one item size, rt_build.cpp
+// rt_host_plan_work, so their register allocation does not carry the decode)
+template <bool kTwoSizes>
 RT_FN bool open_item(const KernelParams& P, int item, ItemCtx& I) {
   const int W = P.cam.width, tile_pixels = P.tile_rows * W;
   I.item = item;
-  // big items first (samples [0, n_big_chunks * big_chunk) of each pixel), then the small ones
-  const bool big = item < P.n_big_items;
-  const int id = big ? item : item - P.n_big_items;
   // item, tile pixel and row are non-negative: exact multiply-shift division by the launch
   // constants instead of the ~20-instruction signed integer division sequences
-  const int k = (int)fast_div((uint32_t)id, P.div_tile);
-  I.tp = id - k * tile_pixels;
+  const int k = (int)fast_div((uint32_t)item, P.div_tile);
+  I.tp = item - k * tile_pixels;
   const int tr = (int)fast_div((uint32_t)I.tp, P.div_width);
   I.px = I.tp - tr * W;
   const int tb = (int)fast_div((uint32_t)tr, P.div_block);
   I.gy = (tb * P.n_shards + P.shard) * P.row_block + (tr - tb * P.row_block);
   I.pix = (uint32_t)(I.gy * W + I.px);
+  // chunks k < n_big_chunks are big (samples [k big_chunk, (k + 1) big_chunk)), the rest small
+  // (from n_big_chunks big_chunk = small_base + n_big_chunks chunk on)
+  const bool big = kTwoSizes && k < P.n_big_chunks;
   const int chunk = big ? P.big_chunk : P.chunk;
-  I.sample = (big ? 0 : P.n_big_chunks * P.big_chunk) + k * chunk;
+  I.sample = (big ? 0 : kTwoSizes ? P.small_base : 0) + k * chunk;
   I.s_end = I.sample + chunk < P.cam.spp ? I.sample + chunk : P.cam.spp;
   if (I.gy >= P.cam.height || P.cam.max_depth <= 0) I.s_end = I.sample;  // padding row / black image
   return I.sample < I.s_end;
@@ -1407,7 +1410,7 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
       if (got >= P.n_items) break;
       acc_clear(acc);
       bad = false;
-      if (!open_item(P, got, I)) continue;
+      if (!open_item<kFlat>(P, got, I)) continue;
     }
     if (!alive) {
       camera_ray(P, I.pix, I.sample, I.px, I.gy, R);
@@ -1507,7 +1510,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
       if (got >= P.n_items) break;
       acc_clear(acc);
       bad = false;
-      state = open_item(P, got, I) ? ST_NEED_SAMPLE : ST_NEED_ITEM;
+      state = open_item<false>(P, got, I) ? ST_NEED_SAMPLE : ST_NEED_ITEM;
     }
     if (state == ST_NEED_SAMPLE) {
       camera_ray(P, I.pix, I.sample, I.px, I.gy, R);

@@ -94,13 +94,14 @@ int render(const HostScene& H, const rt_camera_settings* cs, uint64_t seed, cons
   for (int k = 0; k <= RT_MAX_MEDIA; ++k) P.flat_sets[k] = H.flat_sets[k];
   P.stack_depth = H.max_depth > 1 ? H.max_depth : 1;
   P.n_prims = H.n_prims;
-  rt_host_plan_work(P, 4096);
+  const int variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex, H.n_instances > 0);
+  rt_host_plan_work(P, 4096, (variant & RT_VAR_BASE) == RT_VAR_FLAT);
   P.trav_exit_pct = H.trav_exit_pct;
   if (chunk > 0) {
     P.chunk = chunk;
     P.n_chunks = (P.cam.spp + chunk - 1) / chunk;
     P.n_big_chunks = 0;
-    P.n_big_items = 0;
+    P.small_base = 0;
     P.n_items = P.n_chunks * P.tile_rows * P.cam.width;
   }
   const size_t tile_pixels = (size_t)P.tile_rows * P.cam.width;
@@ -111,7 +112,7 @@ int render(const HostScene& H, const rt_camera_settings* cs, uint64_t seed, cons
   for (auto& f : flags) f = 0;
   Shared s;
   s.P = &P;
-  s.variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex, H.n_instances > 0);
+  s.variant = variant;
   s.accum = &accum;
   s.flags = &flags;
   for (auto& c : s.cnt) c = 0;

@@ -147,12 +147,13 @@ def test_kernel_variants_render_bitwise_identical_images(emu_mod, monkeypatch, n
         assert np.array_equal(img, imgs[0], equal_nan=True)
 
 
-@pytest.mark.parametrize("name", ["cornell", "pawn_fog"])
+@pytest.mark.parametrize("name", ["cornell", "readme"])
 def test_two_size_items_render_the_same_image(emu_mod, monkeypatch, name):
-    """Work items of two sizes (rt_build.cpp rt_host_plan_work: big items for the first samples
-    of every pixel, small ones for the tail; rt_trace.h open_item) cover every (pixel, sample)
-    exactly once: with fixed-point sums the image is bit-identical to one item size."""
-    fn = {"cornell": scenes.cornell_box, "pawn_fog": scenes.pawn_fog}[name]
+    """Work items of two sizes (flat kernel; rt_build.cpp rt_host_plan_work: big items for the
+    first samples of every pixel, small ones for the tail; rt_trace.h open_item) cover every
+    (pixel, sample) exactly once: with fixed-point sums the image is bit-identical to one item
+    size."""
+    fn = {"cornell": scenes.cornell_box, "readme": scenes.readme_scene}[name]
     cs, world, seed = fn(width=40, spp=37)
     a = emu_mod.render(cs, world, seed)
     monkeypatch.setenv("RT_AMD_TAIL_ITEMS", "1")
