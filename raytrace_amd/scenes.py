@@ -190,6 +190,35 @@ def bunny_instances(width=400, spp=64, depth=50, n=3):
     return cornell_settings(width, spp, depth, redirect=True), world, mkStdGen(91)
 
 
+def instance_gallery(width=160, spp=8, depth=20):
+    """Two-level instancing edge cases (test scene, not a reference scene): ONE object with its
+    own leaf materials — a bunny mesh (lambertian), a checker-textured sphere (sphereUV in object
+    space) and a metal parallelogram — placed four times: a rotation, a reflection (x -> -x,
+    det -1: the object's front sides must follow the reference's m-mapped normals), a rotation
+    with a dielectric `<$` over the whole placement (the outermost material wins), and a
+    translation; sky background."""
+    from .geometry import M44
+    mesh = load_mesh("bunny.obj")
+    center = tuple(midpoint(i) for i in boundingBox(triangleMesh(mesh)))
+    obj_mesh = transformVertices(scale(6) @ translate(tuple(-c for c in center)), mesh)
+    obj = group([lambertian(constantTexture(V3(0.8, 0.6, 0.3))) << triangleMesh(obj_mesh),
+                 lambertian(checkerTexture(8, 4, V3(0.9, 0.1, 0.1), V3(0.1, 0.1, 0.9))) << sphere(V3(0.9, 0.3, 0), 0.35),
+                 metal(0.05, constantTexture(V3(0.8, 0.8, 0.8))) << parallelogram(V3(-1, -0.5, -0.8), V3(2, 0, 0),
+                                                                                   V3(0, 1.2, 0))])
+    reflect_x = M44(((-1, 0, 0, 0), (0, 1, 0, 0), (0, 0, 1, 0), (0, 0, 0, 1)))
+    world = group([
+        lambertian(constantTexture(V3(0.5, 0.5, 0.5))) << sphere(V3(0, -1000.6, 0), 1000),
+        transform(translate(V3(-2.2, 0, -1)) @ rotateY(degrees(35)), obj),
+        transform(translate(V3(0, 0, -1.5)) @ reflect_x @ rotateY(degrees(-20)), obj),
+        dielectric(1.5) << transform(translate(V3(2.2, 0, -1)) @ rotateY(degrees(120)), obj),
+        transform(translate(V3(0.3, 0.2, 1.2)), obj),
+    ])
+    settings = defaultCameraSettings(cs_center=V3(0, 1.5, 5), cs_lookAt=V3(0, 0.2, 0), cs_imageWidth=width,
+                                     cs_vfov=degrees(50), cs_samplesPerPixel=spp, cs_maxRecursionDepth=depth,
+                                     cs_background=sky)
+    return settings, world, mkStdGen(17)
+
+
 def pawn_test(width=500, spp=400, depth=20):
     mesh = transformVertices(scale(100), load_mesh("pawn.obj"))
     settings = defaultCameraSettings(cs_center=V3(0, 3.75, 5), cs_lookAt=V3(0, 2.75, 0), cs_imageWidth=width,
@@ -250,4 +279,5 @@ CONFIGS = {
     "noise_test": noise_test,
     "box_gallery": box_gallery,
     "bunny_instances": bunny_instances,
+    "instance_gallery": instance_gallery,
 }

@@ -99,6 +99,7 @@ FULL = [
     ("demo1_1200x800", scenes.demo1_1200x800, dict(spp=2), "cornell", 1.0),
     ("bunny_cornell", scenes.bunny_cornell, dict(spp=4), "cornell", 15.0),
     ("pawn_fog", scenes.pawn_fog, dict(spp=4), "cornell", 1.0),
+    ("bunny_instances", scenes.bunny_instances, dict(spp=4, n=8), "cornell", 15.0),
 ]
 
 
@@ -393,6 +394,19 @@ def test_two_level_instancing_against_oracle(gpu, oracle_mod, n, precision):
     assert_parity(img, ref, precision, 0.99, _floor()["cornell"], f"instances{n}", 8, 15.0)
     baked = R.raytrace(cs, S.flatten(world, instance_min=0), seed, precision=precision)
     assert_parity(baked, ref, precision, 0.99, _floor()["cornell"], f"baked{n}", 8, 15.0)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_instancing_edge_cases_against_oracle(gpu, oracle_mod, precision):
+    """scenes.instance_gallery: placements by rotation, reflection (det -1), under a dielectric
+    `<$`, and translation of one object with a textured sphere, a metal parallelogram and a mesh."""
+    from raytrace_amd import scene as S
+    cs, world, seed = scenes.instance_gallery(width=128, spp=8)
+    flat = S.flatten(world)
+    assert len(flat.instances) == 4
+    ref = oracle_mod.render(cs, world, seed, mode=oracle_mod.RNG_PHILOX)
+    img = R.raytrace(cs, flat, seed, precision=precision)
+    assert_parity(img, ref, precision, 0.99, _floor()["cornell"], "instance_gallery", 8, 1.0)
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])

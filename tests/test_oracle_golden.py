@@ -235,6 +235,26 @@ def test_two_level_instancing_matches_oracle(oracle_mod, emu_mod, n, precision):
         np.testing.assert_allclose(got.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=5e-3)
 
 
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_instancing_edge_cases_match_oracle(oracle_mod, emu_mod, precision):
+    """scenes.instance_gallery: one object with its own leaf materials placed by a rotation, a
+    reflection (det -1), a rotation under a dielectric `<$` and a translation — a textured
+    sphere's uv, the parallelogram's front side under the reflection and the outermost-material
+    rule through instances, against the oracle's walk of the reference's closures."""
+    from raytrace_amd import scene as S
+    cs, world, seed = scenes.instance_gallery(width=96, spp=4)
+    flat = S.flatten(world)
+    assert len(flat.instances) == 4
+    ref = oracle_mod.render(cs, world, seed, mode=oracle_mod.RNG_PHILOX)
+    got = emu_mod.render(cs, flat, seed, precision=precision)
+    if precision == "f64":
+        rel = (np.abs(got - ref) / np.maximum(np.abs(ref), 1e-3)).max(-1)
+        assert (rel <= 1e-9).mean() >= 0.999
+    else:
+        assert pixel_agreement(got, ref) >= 0.99
+    np.testing.assert_allclose(got.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=5e-3)
+
+
 def test_perlin_tables(oracle_mod):
     """The product's Perlin tables: three permutations of 0..255 (Noise.hs:60-92) and the 256
     gradients of Noise.hs:94-98, identical to the oracle's independent C restatement."""
