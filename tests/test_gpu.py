@@ -121,7 +121,7 @@ def test_full_resolution_parity_on_row_subset(gpu, oracle_mod, name, fn, kw, fl,
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 def test_gpu_matches_kernel_emulator(gpu, emu_mod, precision):
     """Same source (rt_trace.h) on the host: identical numbers up to FP contraction / libm (the
-    device's Newton-refined binary64 reciprocals and its sin / cos polynomial differ from the
+    device's refined hardware binary64 reciprocals and its sin / cos polynomial differ from the
     host's IEEE / libm results by ulps)."""
     cs, world, seed = scenes.cornell_box(spp=8, width=64)
     a = R.raytrace(cs, world, seed, precision=precision)

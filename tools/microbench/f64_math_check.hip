@@ -1,5 +1,5 @@
 // f64_math_check.hip — accuracy of the render kernel's binary64 device math (rt_trace.h
-// rt_math64: Newton-refined v_rcp_f64 / v_rsq_f64, sin / cos of 2 pi u) against the IEEE /
+// rt_math64: v_rcp_f64 / v_rsq_f64 with a third-order correction, sin / cos of 2 pi u) against the IEEE /
 // OCML results on the device.  Prints one JSON object: per function the largest difference in
 // units in the last place and the fraction of inputs that differ at all.
 #include <hip/hip_runtime.h>
