@@ -38,6 +38,7 @@
 
 #include "../../include/rt.h"
 #include "rt_internal.h"
+#include "rt_sincos_table.h"
 
 #ifdef RT_HOST_EMU
 #include <cmath>
@@ -166,6 +167,28 @@ __device__ __forceinline__ double sqrt_nonneg(double x) {
   s = __builtin_fma(d, h, s);
   return x == 0.0 || x == __builtin_huge_val() ? x : s;
 }
+#ifndef RT_SINCOS_POLY
+// sin / cos of 2 pi u for u in [0, 1) (the samplers' angles; u has 24 random bits): u = k / 128 +
+// b with k = rint(128 u) and |b| <= 1/256 exact, (sin, cos)(2 pi k / 128) from a correctly rounded
+// table (rt_sincos_table.h, 2 KB, L1-resident), sin / cos (2 pi b) by short Taylor polynomials
+// (|2 pi b| <= 0.0246: truncation < 1e-17), combined by the angle-addition formulas
+__device__ const double rt_sincos_tab[2 * RT_SINCOS_TABLE_N] = RT_SINCOS_TABLE_INIT;
+__device__ __forceinline__ void sincos_turns(double u, double* sn, double* cs) {
+  const double kq = __builtin_rint(u * (double)RT_SINCOS_TABLE_N);
+  const double b = __builtin_fma(kq, -1.0 / RT_SINCOS_TABLE_N, u);
+  const int k = (int)kq & (RT_SINCOS_TABLE_N - 1);
+  const double sa = rt_sincos_tab[2 * k], ca = rt_sincos_tab[2 * k + 1];
+  const double x = b * 6.283185307179586, x2 = x * x;
+  double ps = __builtin_fma(x2, -1.0 / 5040.0, 1.0 / 120.0);
+  ps = __builtin_fma(x2, ps, -1.0 / 6.0);
+  const double sb = __builtin_fma(x2 * x, ps, x);
+  double pc = __builtin_fma(x2, -1.0 / 720.0, 1.0 / 24.0);
+  pc = __builtin_fma(x2, pc, -0.5);
+  const double cb = __builtin_fma(x2, pc, 1.0);
+  *sn = __builtin_fma(sa, cb, ca * sb);
+  *cs = __builtin_fma(ca, cb, -(sa * sb));
+}
+#else
 // sin / cos of 2 pi u for u in [0, 1) (the samplers' angles; u has 24 random bits): the quadrant
 // q = rint(4 u) and r = u - q / 4 in [-1/8, 1/8] are exact, sin / cos (2 pi r) are Taylor
 // polynomials in r (truncation < 1e-18), and the quadrant swaps / negates them
@@ -197,6 +220,7 @@ __device__ __forceinline__ void sincos_turns(double u, double* sn, double* cs) {
   *sn = (k & 2) ? -ss : ss;
   *cs = ((k + 1) & 2) ? -cc : cc;
 }
+#endif
 }  // namespace rt_math64
 #endif
 #endif
