@@ -922,6 +922,7 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
     psum = (k == 0) ? t.prob : psum + t.prob;
     T.prob = (R)t.prob;
     T.thresh = (R)cum;
+    T.prob_icr = (R)(t.prob / ncp);
   }
   P.rem_prob = (R)(1.0 - psum);
   P.key0 = (uint32_t)seed;

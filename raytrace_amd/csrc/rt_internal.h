@@ -182,7 +182,7 @@ struct DevTargetT {
   R cr[3];    // u x v (pdf denominator, Ray.hs:202)
   R prob;
   R thresh;   // cumulative probability (scanl1 (+) probs)
-  R pad;
+  R prob_icr; // prob / |u x v|: the pdf term p t^2 / |(u x v) . dir| = prob_icr t^2 / |n . dir|
 };
 
 // One placement of an instanced object (rt.h rt_instance): object -> world rigid transform,

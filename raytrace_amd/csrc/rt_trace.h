@@ -799,13 +799,14 @@ RT_FN f3 eval_texture(const KernelParams& P, int tex, real u, real v, f3 p) {
   return c0;  // not reached: scenes with noise textures run the kNoise kernels
 }
 
-// rt_hit of a redirect target: parallelogram on (0, infinity) (Ray.hs:143-145)
-RT_FN bool target_hit(const DevTarget& T, f3 o, f3 d, real& t) {
+// rt_hit of a redirect target: parallelogram on (0, infinity) (Ray.hs:143-145); rinv = 1 / (n . d)
+RT_FN bool target_hit(const DevTarget& T, f3 o, f3 d, real& t, real& rinv) {
   f3 n = ld3(T.n);
   real denom = dot(n, d);
   if (!(RABS(denom) > RL(1e-8))) return false;
   f3 qo = ld3(T.q) - o;
-  t = dot(n, qo) * RT_RCP(denom);
+  rinv = RT_RCP(denom);
+  t = dot(n, qo) * rinv;
   if (!(t > RL(0.0))) return false;
   f3 prel = t * d - qo;
   real a = dot(prel, ld3(T.wa)), b = dot(prel, ld3(T.wb));
@@ -1333,9 +1334,10 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
       }
       real mix = RL(0.0);
       for (int k = 0; k < P.n_targets; ++k) {
-        real tt;
-        if (target_hit(P.targets[k], h.p, dir, tt))
-          mix += P.targets[k].prob * (tt * tt * RT_RCP(RABS(dot(ld3(P.targets[k].cr), dir))));
+        // p t^2 / |(u x v) . dir| (Ray.hs:202) with (u x v) . dir = |u x v| (n . dir): the target
+        // test's reciprocal serves both
+        real tt, rinv;
+        if (target_hit(P.targets[k], h.p, dir, tt, rinv)) mix += P.targets[k].prob_icr * (tt * tt * RABS(rinv));
       }
       real pdf = P.rem_prob * pdf1 + mix;
       f3 f = tex;
