@@ -103,6 +103,7 @@ extern thread_local long long counters[4];
 #undef RT_LOG
 #undef RT_RSQRT
 #undef RT_RCP
+#undef RT_RCP_NZ
 #undef RT_SQRT
 #if RT_F64
 // binary64: IEEE division and square root, libm / OCML transcendentals (the oracle's libm calls)
@@ -126,6 +127,7 @@ extern thread_local long long counters[4];
 #define RT_SINCOS_TURNS(x, s, c) (*(s) = sin(6.283185307179586 * (x)), *(c) = cos(6.283185307179586 * (x)))
 #define RT_RSQRT(x) (1.0 / sqrt(x))
 #define RT_RCP(x) (1.0 / (x))
+#define RT_RCP_NZ(x) (1.0 / (x))
 #define RT_SQRT(x) sqrt(x)
 #else
 // Device binary64 math (rt_math64 below): the hardware reciprocal / reciprocal square root
@@ -135,6 +137,7 @@ extern thread_local long long counters[4];
 #define RT_SINCOS_TURNS(x, s, c) rt_math64::sincos_turns(x, s, c)
 #define RT_RSQRT(x) rt_math64::rsqrt(x)
 #define RT_RCP(x) rt_math64::rcp(x)
+#define RT_RCP_NZ(x) rt_math64::rcp_nz(x)
 #define RT_SQRT(x) rt_math64::sqrt_nonneg(x)
 #ifndef RT_MATH64_DEFINED
 #define RT_MATH64_DEFINED
@@ -148,6 +151,14 @@ __device__ __forceinline__ double rcp(double x) {
   const double e = __builtin_fma(-x, r0, 1.0);
   const double r = __builtin_fma(r0, __builtin_fma(e, e, e), r0);
   return r == r ? r : r0;
+}
+// 1 / x where a +-0 / +-inf x need not give +-inf / +-0 (they give NaN): callers whose result is
+// discarded for such x (a plane test's |n . d| <= 1e-8 margin, a redirect target's checked
+// denominator) skip rcp's NaN guard
+__device__ __forceinline__ double rcp_nz(double x) {
+  const double r0 = __builtin_amdgcn_rcp(x);
+  const double e = __builtin_fma(-x, r0, 1.0);
+  return __builtin_fma(r0, __builtin_fma(e, e, e), r0);
 }
 // 1 / sqrt(x), x > 0: v_rsq_f64 and one third-order correction, 1/sqrt(x) = y (1 - e)^(-1/2) =
 // y (1 + e/2 + 3 e^2 / 8 + ...) with e = 1 - x y^2 (within 2 ulp, as two Newton steps were)
@@ -244,6 +255,7 @@ __device__ __forceinline__ void sincos_turns(double u, double* sn, double* cs) {
 #define RT_LOG(x) logf(x)
 #define RT_RSQRT(x) (1.0f / sqrtf(x))
 #define RT_RCP(x) (1.0f / (x))
+#define RT_RCP_NZ(x) (1.0f / (x))
 #define RT_SQRT(x) sqrtf(x)
 #else
 // sin / cos of 2 pi x for x in [0, 1): v_sin_f32 / v_cos_f32 take their argument in turns
@@ -251,6 +263,7 @@ __device__ __forceinline__ void sincos_turns(double u, double* sn, double* cs) {
 #define RT_LOG(x) __logf(x)
 #define RT_RSQRT(x) __frsqrt_rn(x)
 #define RT_RCP(x) __builtin_amdgcn_rcpf(x)
+#define RT_RCP_NZ(x) __builtin_amdgcn_rcpf(x)
 #define RT_SQRT(x) __builtin_amdgcn_sqrtf(x)  // v_sqrt_f32 (1 ulp), no IEEE fix-up sequence
 #endif
 #endif
@@ -512,7 +525,7 @@ RT_FN void isect_plane(const PrimRec& r, f3 o, const RayCtx& R, real tmin_up, bo
   f3 n = xyz(r.a);
   real denom = dot(n, R.d);
   f3 qo = xyz(r.b) - o;
-  t = dot(n, qo) * RT_RCP(denom);
+  t = dot(n, qo) * RT_RCP_NZ(denom);  // |denom| <= 1e-8 (NaN t included) fails the margin m2
   f3 prel = t * R.d - qo;
   real aa = dot(prel, xyz(r.c)), bb = dot(prel, xyz(r.e));
   real m1, m2 = RMIN(RABS(denom) - RL(1e-8), t - tmin_up);
@@ -805,7 +818,7 @@ RT_FN bool target_hit(const DevTarget& T, f3 o, f3 d, real& t, real& rinv) {
   real denom = dot(n, d);
   if (!(RABS(denom) > RL(1e-8))) return false;
   f3 qo = ld3(T.q) - o;
-  rinv = RT_RCP(denom);
+  rinv = RT_RCP_NZ(denom);
   t = dot(n, qo) * rinv;
   if (!(t > RL(0.0))) return false;
   f3 prel = t * d - qo;
