@@ -624,9 +624,33 @@ RT_FN void test_box(const RT_CAS DevBox* B, const RayCtx& R, real tmin_up, Close
                     f3{B->a2[0], B->a2[1], B->a2[2]}};
   real lo[3], hi[3];
   int flip[3];
+#if RT_F64 && !defined(RT_BOX_THREE_RCP)
+  // Binary64: the three slab reciprocals from ONE reciprocal of their product, 1 / d_k =
+  // (d_i d_j) / (d_0 d_1 d_2) — one v_rcp_f64 and its correction instead of three (within ~4 ulp
+  // of 1 / d_k).  A product that is zero, denormal or infinite (an axis parallel to the ray)
+  // takes the three guarded reciprocals instead, a branch no lane normally enters.
+  real dk[3], invk[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) dk[k] = dot(ax[k], R.d);
+  {
+    const real d01 = dk[0] * dk[1], p = d01 * dk[2];
+    const real r = RT_RCP_NZ(p);
+    invk[0] = r * (dk[1] * dk[2]);
+    invk[1] = r * (dk[0] * dk[2]);
+    invk[2] = r * d01;
+    if (!(RABS(p) >= RL(1e-300) && RABS(p) <= RL(1e300))) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) invk[k] = RT_RCP(dk[k]);
+    }
+  }
+#endif
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
+#if RT_F64 && !defined(RT_BOX_THREE_RCP)
+    const real inv = invk[k];
+#else
     const real inv = RT_RCP(dot(ax[k], R.d));
+#endif
     const real s = dot(ax[k], oc);
     const real t0 = -s * inv, t1 = RFMA(-s, inv, inv);  // the s = 0 and s = 1 planes
     flip[k] = t1 < t0 ? 1 : 0;                            // entering through the s = 1 end
