@@ -396,8 +396,24 @@ RT_FN f3 unit_vector(uint32_t a, uint32_t b) {
   return mk3(r * c, r * s, z);
 }
 
+// Binary64 kernels test BVH nodes in FP32 (the node boxes are floats; RT_NODE_F64 restores the
+// binary64 slab test): the ray carries 1 / d and two offsets, o / d plus and minus a rounding pad,
+// so the FP32 slab interval contains the exact one (prep_ray, trav_round).
+#if RT_F64 && !defined(RT_NODE_F64)
+#define RT_NODE_F32 1
+struct f3n {
+  float x, y, z;
+};
+#else
+#define RT_NODE_F32 0
+#endif
 struct RayCtx {
-  f3 o, d, idir, oidir;
+  f3 o, d;
+#if RT_NODE_F32
+  f3n idir, off0, off1;  // 1 / d; o / d for the box-min planes (off0) and the box-max planes (off1)
+#else
+  f3 idir, oidir;
+#endif
   real time;
   int self_gid;   // the leaf the ray leaves (skipped: FP32 robustness, rt_trace.h isect_*)
   int self_inst;  // ... and its instance (-1: a world leaf; two-level instancing, RT_VAR_INST)
@@ -417,10 +433,32 @@ RT_FN f3 motion_shift(const KernelParams& P, int m, real time) {
 RT_FN real safe_rcp(real d) { return RT_RCP(RABS(d) > RL(1e-20) ? d : RCOPYSIGN(RL(1e-20), d)); }
 
 // reciprocal direction and origin x reciprocal for the BVH slab tests
+#if RT_NODE_F32
+// One axis of the FP32 node ray.  t = b (1/d) - o/d in FP32 is off the exact (b - o) / d by at
+// most ~3 eps |o/d| (rounding of 1/d and o/d to float, the offset's own rounding) plus ~2 eps |t|
+// (the fma, and 1/d's rounding times b/d): pad = 5 eps |o/d| moves the entry plane down and the
+// exit plane up (which plane enters follows the sign of 1/d), and trav_round widens the far end
+// by (1 + 2^-20) for the relative part.
+RT_FN void prep_axis(real o, real d, float& fi, float& f0, float& f1) {
+  const real i = safe_rcp(d);
+  const float oi = (float)(o * i);
+  const float pad = 3.0e-7f * fabsf(oi);
+  const float sp = i >= RL(0.0) ? pad : -pad;
+  fi = (float)i;
+  f0 = oi + sp;  // box-min plane: the entry when 1/d >= 0 (its t lowered)
+  f1 = oi - sp;  // box-max plane
+}
+RT_FN void prep_ray(RayCtx& R) {
+  prep_axis(R.o.x, R.d.x, R.idir.x, R.off0.x, R.off1.x);
+  prep_axis(R.o.y, R.d.y, R.idir.y, R.off0.y, R.off1.y);
+  prep_axis(R.o.z, R.d.z, R.idir.z, R.off0.z, R.off1.z);
+}
+#else
 RT_FN void prep_ray(RayCtx& R) {
   R.idir = mk3(safe_rcp(R.d.x), safe_rcp(R.d.y), safe_rcp(R.d.z));
   R.oidir = R.o * R.idir;
 }
+#endif
 
 // Two-level instancing (rt_internal.h DevInstance): world -> object space through the inverse of
 // the rigid placement (R^T (p - t); t is unchanged along the ray) and object -> world normals.
@@ -1032,6 +1070,19 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
       cl = n3p->x;
       cr = n3p->y;
     }
+#if RT_NODE_F32
+    const float tminf = (float)S.tmin, ctf = (float)S.C.t;
+    float lx0 = fmaf(n0.x, R.idir.x, -R.off0.x), lx1 = fmaf(n0.y, R.idir.x, -R.off1.x);
+    float ly0 = fmaf(n0.z, R.idir.y, -R.off0.y), ly1 = fmaf(n0.w, R.idir.y, -R.off1.y);
+    float lz0 = fmaf(n2.x, R.idir.z, -R.off0.z), lz1 = fmaf(n2.y, R.idir.z, -R.off1.z);
+    float rx0 = fmaf(n1.x, R.idir.x, -R.off0.x), rx1 = fmaf(n1.y, R.idir.x, -R.off1.x);
+    float ry0 = fmaf(n1.z, R.idir.y, -R.off0.y), ry1 = fmaf(n1.w, R.idir.y, -R.off1.y);
+    float rz0 = fmaf(n2.z, R.idir.z, -R.off0.z), rz1 = fmaf(n2.w, R.idir.z, -R.off1.z);
+    const float lnear = fmaxf(fmaxf(fminf(lx0, lx1), fminf(ly0, ly1)), fmaxf(fminf(lz0, lz1), tminf));
+    const float lfar = fminf(fminf(fmaxf(lx0, lx1), fmaxf(ly0, ly1)), fminf(fmaxf(lz0, lz1), ctf)) * 1.00000095f;
+    const float rnear = fmaxf(fmaxf(fminf(rx0, rx1), fminf(ry0, ry1)), fmaxf(fminf(rz0, rz1), tminf));
+    const float rfar = fminf(fminf(fmaxf(rx0, rx1), fmaxf(ry0, ry1)), fminf(fmaxf(rz0, rz1), ctf)) * 1.00000095f;
+#else
     real lx0 = RFMA(n0.x, R.idir.x, -R.oidir.x), lx1 = RFMA(n0.y, R.idir.x, -R.oidir.x);
     real ly0 = RFMA(n0.z, R.idir.y, -R.oidir.y), ly1 = RFMA(n0.w, R.idir.y, -R.oidir.y);
     real lz0 = RFMA(n2.x, R.idir.z, -R.oidir.z), lz1 = RFMA(n2.y, R.idir.z, -R.oidir.z);
@@ -1042,7 +1093,7 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
     real lfar = RMIN(RMIN(RMAX(lx0, lx1), RMAX(ly0, ly1)), RMIN(RMAX(lz0, lz1), S.C.t));
     real rnear = RMAX(RMAX(RMIN(rx0, rx1), RMIN(ry0, ry1)), RMAX(RMIN(rz0, rz1), S.tmin));
     real rfar = RMIN(RMIN(RMAX(rx0, rx1), RMAX(ry0, ry1)), RMIN(RMAX(rz0, rz1), S.C.t));
-#ifdef RT_EXP_DOUBLE_NODE  // ablation: the slab tests computed twice (marginal cost of a node visit)
+#ifdef RT_EXP_DOUBLE_NODE  // (binary64 node test only)  // ablation: the slab tests computed twice (marginal cost of a node visit)
     {
       const real e = (real)P.cam.pad;
       real ax0 = RFMA(n0.x + e, R.idir.x, -R.oidir.x), ax1 = RFMA(n0.y + e, R.idir.x, -R.oidir.x);
@@ -1056,6 +1107,7 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
       rnear = RMIN(rnear, RMAX(RMAX(RMIN(bx0, bx1), RMIN(by0, by1)), RMAX(RMIN(bz0, bz1), S.tmin)));
       rfar = RMAX(rfar, RMIN(RMIN(RMAX(bx0, bx1), RMAX(by0, by1)), RMIN(RMAX(bz0, bz1), S.C.t)));
     }
+#endif
 #endif
     const bool hl = lnear <= lfar, hr = rnear <= rfar;
 #ifndef RT_BRANCHY_STACK
@@ -1459,7 +1511,12 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
   bool alive = false;
   f3 L = mk3(RL(0.), RL(0.), RL(0.)), T = mk3(RL(1.), RL(1.), RL(1.));
   RayCtx R;
-  R.o = R.d = R.idir = R.oidir = L;
+  R.o = R.d = L;
+#if RT_NODE_F32
+  R.idir = R.off0 = R.off1 = f3n{0.f, 0.f, 0.f};
+#else
+  R.idir = R.oidir = L;
+#endif
   R.time = RL(0.0);
   R.self_gid = -1;
   R.self_inst = -1;
@@ -1550,7 +1607,12 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
   int state = ST_NEED_ITEM;
   f3 L = mk3(RL(0.), RL(0.), RL(0.)), T = mk3(RL(1.), RL(1.), RL(1.));
   RayCtx R;
-  R.o = R.d = R.idir = R.oidir = L;
+  R.o = R.d = L;
+#if RT_NODE_F32
+  R.idir = R.off0 = R.off1 = f3n{0.f, 0.f, 0.f};
+#else
+  R.idir = R.oidir = L;
+#endif
   R.time = RL(0.0);
   R.self_gid = -1;
   R.self_inst = -1;
