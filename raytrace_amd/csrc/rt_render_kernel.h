@@ -145,15 +145,19 @@ struct AtomicCommit {
 #define RT_WAVES64_FLAT 2  // readme f64 0.87 -> 0.78 ms at 2 (4: 1.31); the BVH kernels keep 3 (2: demo1 +23 %, pawn+fog +17 %)
 #endif
 #ifndef RT_WAVES64_BVH_LITE
-#define RT_WAVES64_BVH_LITE 3
+#define RT_WAVES64_BVH_LITE 4  // 163 ms bunny-Cornell vs 180 at 3 once the BVH nodes were tested in FP32 (profiles/r2/waves64)
 #endif
 #ifndef RT_WAVES64_BVH
-#define RT_WAVES64_BVH 3
+#define RT_WAVES64_BVH 4  // demo1 69.9 ms vs 76.6 at 3 (profiles/r2/waves64)
+#endif
+#ifndef RT_WAVES64_BVH_MEDIA
+#define RT_WAVES64_BVH_MEDIA 3  // the media kernels spill more: pawn+fog 641 ms at 3, 883 at 4
 #endif
 #if RT_F64
 #define RT_WAVES_OF(kVar, kTex, kMedia, kMats)                                                     \
   ((kVar) == RT_VAR_FLAT ? ((kTex) == 0 && !(kMedia) && !(kMats) ? RT_WAVES64_FLAT_LITE : RT_WAVES64_FLAT) \
-                         : ((kTex) == 0 && !(kMedia) && !(kMats) ? RT_WAVES64_BVH_LITE : RT_WAVES64_BVH))
+                         : (kMedia) ? RT_WAVES64_BVH_MEDIA                                          \
+                         : ((kTex) == 0 && !(kMats) ? RT_WAVES64_BVH_LITE : RT_WAVES64_BVH))
 #else
 #define RT_WAVES_OF(kVar, kTex, kMedia, kMats)                                                           \
   ((kVar) == RT_VAR_FLAT ? ((kTex) == 2 ? RT_WAVES_FLAT_NOISE : (kTex) == 0 ? RT_WAVES_FLAT_TEX0 : RT_WAVES_FLAT) \
