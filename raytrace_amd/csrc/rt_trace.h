@@ -453,6 +453,23 @@ RT_FN void prep_ray(RayCtx& R) {
   prep_axis(R.o.y, R.d.y, R.idir.y, R.off0.y, R.off1.y);
   prep_axis(R.o.z, R.d.z, R.idir.z, R.off0.z, R.off1.z);
 }
+// The two children's slab intervals of one BVH node (n0 = left x / y bounds, n1 = right x / y,
+// n2 = left z, right z; min before max) against (tmin, t_closest); a child is entered when its
+// near <= far.  tests/test_host_mirror.py checks on the host emulator that this accepts every box
+// the exact slab test accepts.
+RT_FN void node_slabs_f32(const RayCtx& R, const v4f& n0, const v4f& n1, const v4f& n2, float tminf, float ctf,
+                          float& lnear, float& lfar, float& rnear, float& rfar) {
+  const float lx0 = fmaf(n0.x, R.idir.x, -R.off0.x), lx1 = fmaf(n0.y, R.idir.x, -R.off1.x);
+  const float ly0 = fmaf(n0.z, R.idir.y, -R.off0.y), ly1 = fmaf(n0.w, R.idir.y, -R.off1.y);
+  const float lz0 = fmaf(n2.x, R.idir.z, -R.off0.z), lz1 = fmaf(n2.y, R.idir.z, -R.off1.z);
+  const float rx0 = fmaf(n1.x, R.idir.x, -R.off0.x), rx1 = fmaf(n1.y, R.idir.x, -R.off1.x);
+  const float ry0 = fmaf(n1.z, R.idir.y, -R.off0.y), ry1 = fmaf(n1.w, R.idir.y, -R.off1.y);
+  const float rz0 = fmaf(n2.z, R.idir.z, -R.off0.z), rz1 = fmaf(n2.w, R.idir.z, -R.off1.z);
+  lnear = fmaxf(fmaxf(fminf(lx0, lx1), fminf(ly0, ly1)), fmaxf(fminf(lz0, lz1), tminf));
+  lfar = fminf(fminf(fmaxf(lx0, lx1), fmaxf(ly0, ly1)), fminf(fmaxf(lz0, lz1), ctf)) * 1.00000095f;
+  rnear = fmaxf(fmaxf(fminf(rx0, rx1), fminf(ry0, ry1)), fmaxf(fminf(rz0, rz1), tminf));
+  rfar = fminf(fminf(fmaxf(rx0, rx1), fmaxf(ry0, ry1)), fminf(fmaxf(rz0, rz1), ctf)) * 1.00000095f;
+}
 #else
 RT_FN void prep_ray(RayCtx& R) {
   R.idir = mk3(safe_rcp(R.d.x), safe_rcp(R.d.y), safe_rcp(R.d.z));
@@ -1071,17 +1088,8 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
       cr = n3p->y;
     }
 #if RT_NODE_F32
-    const float tminf = (float)S.tmin, ctf = (float)S.C.t;
-    float lx0 = fmaf(n0.x, R.idir.x, -R.off0.x), lx1 = fmaf(n0.y, R.idir.x, -R.off1.x);
-    float ly0 = fmaf(n0.z, R.idir.y, -R.off0.y), ly1 = fmaf(n0.w, R.idir.y, -R.off1.y);
-    float lz0 = fmaf(n2.x, R.idir.z, -R.off0.z), lz1 = fmaf(n2.y, R.idir.z, -R.off1.z);
-    float rx0 = fmaf(n1.x, R.idir.x, -R.off0.x), rx1 = fmaf(n1.y, R.idir.x, -R.off1.x);
-    float ry0 = fmaf(n1.z, R.idir.y, -R.off0.y), ry1 = fmaf(n1.w, R.idir.y, -R.off1.y);
-    float rz0 = fmaf(n2.z, R.idir.z, -R.off0.z), rz1 = fmaf(n2.w, R.idir.z, -R.off1.z);
-    const float lnear = fmaxf(fmaxf(fminf(lx0, lx1), fminf(ly0, ly1)), fmaxf(fminf(lz0, lz1), tminf));
-    const float lfar = fminf(fminf(fmaxf(lx0, lx1), fmaxf(ly0, ly1)), fminf(fmaxf(lz0, lz1), ctf)) * 1.00000095f;
-    const float rnear = fmaxf(fmaxf(fminf(rx0, rx1), fminf(ry0, ry1)), fmaxf(fminf(rz0, rz1), tminf));
-    const float rfar = fminf(fminf(fmaxf(rx0, rx1), fmaxf(ry0, ry1)), fminf(fmaxf(rz0, rz1), ctf)) * 1.00000095f;
+    float lnear, lfar, rnear, rfar;
+    node_slabs_f32(R, n0, n1, n2, (float)S.tmin, (float)S.C.t, lnear, lfar, rnear, rfar);
 #else
     real lx0 = RFMA(n0.x, R.idir.x, -R.oidir.x), lx1 = RFMA(n0.y, R.idir.x, -R.oidir.x);
     real ly0 = RFMA(n0.z, R.idir.y, -R.oidir.y), ly1 = RFMA(n0.w, R.idir.y, -R.oidir.y);

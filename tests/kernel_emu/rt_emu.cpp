@@ -47,6 +47,23 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
 }
 
 extern "C" {
+// The binary64 kernel's FP32 BVH node test (rtk64::prep_ray + node_slabs_f32) for n rays, each
+// against one box given as both children of a node: box = (xmin, xmax, ymin, ymax, zmin, zmax)
+// floats, o / d / (tmin, tmax) doubles; accept[i] = 1 when the kernel would enter the box.
+void rt_emu_node_test_f64(int n, const double* o, const double* d, const float* box, const double* tr, int* accept) {
+  for (int i = 0; i < n; ++i) {
+    rtk64::RayCtx R{};
+    R.o = rtk64::f3{o[3 * i], o[3 * i + 1], o[3 * i + 2]};
+    R.d = rtk64::f3{d[3 * i], d[3 * i + 1], d[3 * i + 2]};
+    rtk64::prep_ray(R);
+    const float* b = box + 6 * i;
+    const rtk64::v4f n0{b[0], b[1], b[2], b[3]}, n1{b[0], b[1], b[2], b[3]}, n2{b[4], b[5], b[4], b[5]};
+    float ln, lf, rn, rf;
+    rtk64::node_slabs_f32(R, n0, n1, n2, (float)tr[2 * i], (float)tr[2 * i + 1], ln, lf, rn, rf);
+    accept[i] = (ln <= lf ? 1 : 0) | (rn <= rf ? 2 : 0);
+  }
+}
+
 // scene summary of the host build (test tooling): n_nodes, surface_nodes, max_depth, n_prims, flat
 int rt_emu_scene_info(const rt_scene* sc, int* info) {
   HostScene H;
