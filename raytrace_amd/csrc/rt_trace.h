@@ -439,11 +439,26 @@ RT_FN real safe_rcp(real d) { return RT_RCP(RABS(d) > RL(1e-20) ? d : RCOPYSIGN(
 // (the fma, and 1/d's rounding times b/d): pad = 5 eps |o/d| moves the entry plane down and the
 // exit plane up (which plane enters follows the sign of 1/d), and trav_round widens the far end
 // by (1 + 2^-20) for the relative part.
+#ifndef RT_RCPF
+#ifdef RT_HOST_EMU
+#define RT_RCPF(x) (1.0f / (x))
+#else
+#define RT_RCPF(x) __builtin_amdgcn_rcpf(x)
+#endif
+#endif
 RT_FN void prep_axis(real o, real d, float& fi, float& f0, float& f1) {
+#ifndef RT_NODE_RCP64
+  // FP32 reciprocal of the (clamped) direction: t = (b - o) fi is then t (1 + delta), |delta| <=
+  // ~3 eps (rounding of d, v_rcp_f32), inside the far end's (1 + 2^-20) margin; o fi in binary64
+  // keeps the offset consistent with fi
+  const float i = RT_RCPF((float)(RABS(d) > RL(1e-20) ? d : RCOPYSIGN(RL(1e-20), d)));
+  const float oi = (float)(o * (real)i);
+#else
   const real i = safe_rcp(d);
   const float oi = (float)(o * i);
+#endif
   const float pad = 3.0e-7f * fabsf(oi);
-  const float sp = i >= RL(0.0) ? pad : -pad;
+  const float sp = i >= 0 ? pad : -pad;
   fi = (float)i;
   f0 = oi + sp;  // box-min plane: the entry when 1/d >= 0 (its t lowered)
   f1 = oi - sp;  // box-max plane
