@@ -470,7 +470,7 @@ RT_FN void prep_ray(RayCtx& R) {
 }
 // The two children's slab intervals of one BVH node (n0 = left x / y bounds, n1 = right x / y,
 // n2 = left z, right z; min before max) against (tmin, t_closest); a child is entered when its
-// near <= far.  tests/test_host_mirror.py checks on the host emulator that this accepts every box
+// near <= far.  tests/test_node_test.py checks on the host emulator that this accepts every box
 // the exact slab test accepts.
 RT_FN void node_slabs_f32(const RayCtx& R, const v4f& n0, const v4f& n1, const v4f& n2, float tminf, float ctf,
                           float& lnear, float& lfar, float& rnear, float& rfar) {

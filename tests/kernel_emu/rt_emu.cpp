@@ -11,6 +11,20 @@
 
 #include "../../include/rt.h"
 #include "../../raytrace_amd/csrc/rt_internal.h"
+// The device's FP32 reciprocal (v_rcp_f32) is within 1 ulp of 1/x, not correctly rounded:
+// rt_emu_set_rcp_ulps(k) makes the emulator's reciprocal the IEEE result moved k ulps (k < 0:
+// toward -inf), so the node test's conservativeness check covers both roundings the device can
+// produce (tests/test_node_test.py).
+namespace rt_emu {
+int rcp_ulps = 0;
+}
+static inline float rt_emu_rcpf(float x) {
+  float r = 1.0f / x;
+  for (int k = rt_emu::rcp_ulps; k > 0; --k) r = std::nextafter(r, HUGE_VALF);
+  for (int k = rt_emu::rcp_ulps; k < 0; ++k) r = std::nextafter(r, -HUGE_VALF);
+  return r;
+}
+#define RT_RCPF(x) rt_emu_rcpf(x)
 #define RT_F64 0
 #include "../../raytrace_amd/csrc/rt_trace.h"
 namespace emu32 {
@@ -47,6 +61,8 @@ int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t see
 }
 
 extern "C" {
+void rt_emu_set_rcp_ulps(int k) { rt_emu::rcp_ulps = k; }
+
 // The binary64 kernel's FP32 BVH node test (rtk64::prep_ray + node_slabs_f32) for n rays, each
 // against one box given as both children of a node: box = (xmin, xmax, ymin, ymax, zmin, zmax)
 // floats, o / d / (tmin, tmax) doubles; accept[i] = 1 when the kernel would enter the box.

@@ -56,8 +56,11 @@ def make_cases(n, seed):
     return o, d, box, tr
 
 
+@pytest.mark.parametrize("rcp_ulps", [-1, 0, 1])
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_fp32_node_test_is_conservative(emu_mod, seed):
+def test_fp32_node_test_is_conservative(emu_mod, seed, rcp_ulps):
+    """rcp_ulps: the direction reciprocal rounded as IEEE (0) or 1 ulp either way (+-1) — the
+    device's v_rcp_f32 is within 1 ulp, so both of its possible results are covered."""
     L = emu_mod.lib()
     f = L.rt_emu_node_test_f64
     f.restype = None
@@ -65,8 +68,12 @@ def test_fp32_node_test_is_conservative(emu_mod, seed):
     o, d, box, tr = make_cases(n, seed)
     acc = np.zeros(n, np.int32)
     dp = ctypes.POINTER(ctypes.c_double)
-    f(n, o.ctypes.data_as(dp), d.ctypes.data_as(dp), box.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
-      tr.ctypes.data_as(dp), acc.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    L.rt_emu_set_rcp_ulps(rcp_ulps)
+    try:
+        f(n, o.ctypes.data_as(dp), d.ctypes.data_as(dp), box.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+          tr.ctypes.data_as(dp), acc.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    finally:
+        L.rt_emu_set_rcp_ulps(0)
     assert np.all((acc == 0) | (acc == 3)), "the two children (the same box) must agree"
     n_exact = n_clear_miss = n_clear_rejected = 0
     for i in range(n):
