@@ -188,6 +188,31 @@ def roofline_of(config, precision, kernel_ms, launch_ms, share, samples_per_laun
     return r
 
 
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: run this same command as N ranks under
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) and return its exit code.
+    Called before this process touches a GPU (counting devices does not initialise one), and the
+    ranks are CHILD processes: nothing is exec'd over a process that has initialised the GPU.
+    Refuses (non-zero exit, no measurement) when fewer than N GPUs are visible, unless
+    RT_BENCH_ONE_DEVICE=1 maps every rank to device 0 (the one-GPU rehearsal)."""
+    import socket
+    import subprocess
+    import torch
+    have = torch.cuda.device_count()
+    if have < n and os.environ.get("RT_BENCH_ONE_DEVICE") != "1":
+        log(f"bench.py: --gpus {n} but only {have} GPU(s) visible; not measuring")
+        return 2
+    with socket.socket() as s:  # a free rendezvous port
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"bench.py: launching {n} ranks: {' '.join(cmd)}")
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -210,10 +235,24 @@ def main():
                          "many seconds (the per-frame time settles after a few hundred ms); 0: exactly W")
     ap.add_argument("--sim-shards", type=int, default=1,
                     help="diagnostic, one process: render only shard 0 of N (one rank's share of an N-GPU frame)")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+    ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="nccl (= RCCL, the real path); gloo gathers through host memory (N>1 rehearsal on one "
-                         "GPU, with RT_BENCH_ONE_DEVICE=1 mapping every rank to device 0)")
+                         "GPU, with RT_BENCH_ONE_DEVICE=1 mapping every rank to device 0); auto: gloo with "
+                         "RT_BENCH_ONE_DEVICE=1, else nccl")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no external launcher: start one rank per GPU ourselves (before anything touches a GPU)
+        raise SystemExit(spawn_ranks(args.gpus))
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_size != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world_size} ranks; "
+                         f"refusing to report a different GPU count than requested")
+    one_device = os.environ.get("RT_BENCH_ONE_DEVICE") == "1"
+    if args.dist_backend == "auto":
+        # RCCL refuses two ranks on one GPU: the one-device rehearsal gathers through gloo
+        args.dist_backend = "gloo" if one_device else "nccl"
 
     import torch
     import torch.distributed as dist
@@ -222,15 +261,14 @@ def main():
     from raytrace_amd.camera import image_height
     from raytrace_amd.ray import DeviceScene, assemble_shards, shard_row_index, shard_rows
 
-    world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world_size != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world_size}; using WORLD_SIZE")
     n = world_size
     n_sh, sh = (args.sim_shards, 0) if world_size == 1 and args.sim_shards > 1 else (n, rank)
-    if os.environ.get("RT_BENCH_ONE_DEVICE") == "1":
+    if one_device:
         local_rank = 0
+    elif torch.cuda.device_count() <= local_rank:
+        raise SystemExit(f"bench.py: rank {rank} needs GPU {local_rank} but {torch.cuda.device_count()} are visible")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if n > 1:
@@ -349,8 +387,11 @@ def main():
                 img = assemble_shards(parts, h, args.row_block)
             else:
                 img = tiles[last][:h].cpu().numpy() if n_sh == 1 else tiles[last].cpu().numpy()
+            import hashlib
             check = {"finite": bool(np.isfinite(img).all()),
-                     "mean_rgb": [round(float(x), 5) for x in img.reshape(-1, 3).mean(0)]}
+                     "mean_rgb": [round(float(x), 5) for x in img.reshape(-1, 3).mean(0)],
+                     # digest of the assembled frame's bytes: equal across GPU counts (bit-identical)
+                     "sha16": hashlib.sha256(np.ascontiguousarray(img).tobytes()).hexdigest()[:16]}
         return dict(elapsed=elapsed, launch_ms=launch_ms, kernel_ms=kernel_ms, warm_frames=warm_frames,
                     warm_s=warm_s, check=check, streams=len(streams))
 
