@@ -1,7 +1,10 @@
+{-# LANGUAGE DataKinds #-}
 {-# LANGUAGE DeriveFunctor #-}
 {-# LANGUAGE ForeignFunctionInterface #-}
+{-# LANGUAGE PatternSynonyms #-}
 {-# LANGUAGE RecordWildCards #-}
 {-# LANGUAGE ScopedTypeVariables #-}
+{-# LANGUAGE ViewPatterns #-}
 -- | MI355X drop-in for 'Graphics.Ray.raytrace' (reference: src/Graphics/Ray.hs:121-238).
 --
 -- Switch a program from the CPU ray tracer to the GPU by importing this module instead of
@@ -14,7 +17,12 @@
 -- 'lambertian', 'dielectric', 'checkerTexture', ...).  The reference's geometries, materials
 -- and textures are closures (Geometry.hs:42, Material.hs:17, Texture.hs:15), which the device
 -- cannot evaluate, so every value built here carries BOTH the reference closure (built by the
--- reference's own constructor) and a description of what it is.  'raytrace' flattens the
+-- reference's own constructor) and a description of what it is.  The reference's raw
+-- constructors are exported under the same names ('Geometry', 'Material', 'Texture': bundled
+-- pattern synonyms with the reference's fields), so user-defined geometries, materials and
+-- textures compile unchanged; they carry no description and render through the CPU fallback
+-- ('fromReferenceGeometry', 'fromReferenceMaterial' and 'fromReferenceTexture' lift existing
+-- reference values the same way).  'raytrace' flattens the
 -- description into the records of include/rt.h and calls rt_render (binary64, every visible
 -- GPU); when any part of the scene is an arbitrary closure ('solidTexture', 'uvTexture',
 -- 'planeShape' with a user predicate, a background that is not @const c@ or a y-lerp, a
@@ -31,17 +39,22 @@ module Graphics.Ray.Device
   ( -- * The drop-in
     raytrace, raytraceWith, DeviceOptions(..), defaultDeviceOptions, Precision(..), RenderError(..)
   , renderOnDevice, deviceCount
+    -- * 8-bit output encoded on the device (writeImage / writeImageSqrt of a render, Ray.hs:248-260)
+  , Encoding(..), renderImage8, raytraceToFile
     -- * Geometry (Geometry.hs:5-16)
-  , Geometry, boundingBox, pureGeometry, transform, moving
+  , Geometry(Geometry), boundingBox, pureGeometry, transform, moving
   , sphere, planeShape, parallelogram, cuboid, triangle, triangleMesh, constantMedium
   , group, bvhNode, bvhTree
     -- * Materials (Material.hs:3-6)
-  , Material, lightSource, pitchBlack, lambertian, lommelSeeliger, mirror, metal, dielectric, transparent
+  , Material(Material), R.MaterialResult(..)
+  , lightSource, pitchBlack, lambertian, lommelSeeliger, mirror, metal, dielectric, transparent
   , isotropic, anisotropic
     -- * Textures (Texture.hs:2-5)
-  , Texture, constantTexture, solidTexture, uvTexture, imageTexture, checkerTexture, noiseTexture, marbleTexture
-    -- * The reference values behind them
+  , Texture(Texture), constantTexture, solidTexture, uvTexture, imageTexture, checkerTexture, noiseTexture
+  , marbleTexture
+    -- * Between the reference's values and these
   , toReference, referenceMaterial, referenceTexture
+  , fromReferenceGeometry, fromReferenceMaterial, fromReferenceTexture
     -- * Unchanged from the reference
   , R.CameraSettings(..), R.defaultCameraSettings, R.ToRandom, R.Mesh(R.Mesh), R.transformVertices, R.parseObj
   , R.readObj, R.translate, R.rotateX, R.rotateY, R.rotateZ, R.scale, R.readImage, R.writeImage, R.writeImageSqrt
@@ -58,20 +71,22 @@ import Data.List (sortOn)
 import Data.Functor.Identity (Identity)
 import Data.Int (Int32)
 import qualified Data.Map.Strict as Map
-import Data.Word (Word64)
+import Data.Word (Word64, Word8)
 import qualified Data.Massiv.Array as A
 import qualified Data.Massiv.Array.Unsafe as AU
 import Foreign
 import Foreign.C.String (CString, peekCString)
 import Foreign.C.Types (CDouble, CFloat, CInt (..))
+import Graphics.Pixel.ColorSpace (Linearity (NonLinear), SRGB)
+import qualified Graphics.Pixel.ColorSpace as C
+import qualified Data.Massiv.Array.IO as I
+import Data.IORef (modifyIORef', newIORef, readIORef, writeIORef)
+import System.Mem.StableName (StableName, eqStableName, hashStableName, makeStableName)
 import Linear (M44, V2 (V2), V3 (V3), V4 (V4), cross, dot, norm, (!*))
 import System.IO.Unsafe (unsafePerformIO)
 import System.Random (StdGen, mkStdGen)
 import System.Random.Internal (StdGen (unStdGen))
 import System.Random.SplitMix (unseedSMGen)
--- Noise.hs:52-86's permutation tables: the one change this binding asks of the reference is to
--- add them to Graphics.Ray.Noise's export list (INTEGRATION.md §3)
-import Graphics.Ray.Noise (permX, permY, permZ)
 
 -- ===================================================================== descriptions
 
@@ -101,37 +116,71 @@ texKey t = case t of
 
 -- | A material (Material.hs:41-129): the reference closure and, when its texture is reifiable,
 -- its kind (rt.h RT_MAT_*), texture and parameter.
-data Material = Material
+data Material = DeviceMaterial
   { matDesc :: Maybe (Int32, TexD, Double)
   , matRef :: R.Material
   }
 
 -- | A texture: the reference closure and, for the reifiable constructors, its description.
-data Texture = Texture
+data Texture = DeviceTexture
   { texDesc :: Maybe TexD
   , texRef :: R.Texture
   }
 
 -- | The geometry tree as written (Geometry.hs:5-16): `group`, `bvhNode` and `bvhTree` are all
 -- closest-hit groups (their result does not depend on the tree's shape, only on the
--- depth-first order of the leaves), `<$` is 'fmap'.
+-- depth-first order of the leaves), `<$` is 'fmap'.  'DPlaced' is a `transform` tagged with the
+-- identity of its child value (tagShared), so that placements of one shared object can share
+-- one object-space BVH on the device.
 data Desc a
   = DSphere Point3 Double a
   | DPlane Int32 Point3 Vec3 Vec3 (V2 Double) (V2 Double) (V2 Double) a  -- ^ rt.h kind 1 / 2
   | DGroup [Desc a]
   | DTransform (M44 Double) (Desc a)
+  | DPlaced Int (M44 Double) (Desc a)
   | DMoving Vec3 Vec3 (Desc a)
   | DMedium Double (Desc ()) a
   deriving (Functor)
 
 -- | A geometry: the reference value and, when every part is reifiable, its description.
-data Geometry m a = Geometry
+data Geometry m a = DeviceGeometry
   { geoDesc :: Maybe (Desc a)
   , geoRef :: R.Geometry m a
   }
 
 instance Functor m => Functor (Geometry m) where
-  fmap f (Geometry d g) = Geometry (fmap (fmap f) d) (fmap f g)
+  fmap f (DeviceGeometry d g) = DeviceGeometry (fmap (fmap f) d) (fmap f g)
+
+-- | The reference's raw constructor (Geometry.hs:42): a user-defined geometry, rendered on the
+-- CPU (its hit function is a closure).  Matching on it yields the reference value's fields.
+pattern Geometry :: Box -> (Double -> Ray -> Interval -> m (Maybe (HitRecord, a))) -> Geometry m a
+pattern Geometry box hit <- (geoRef -> R.Geometry box hit)
+  where Geometry box hit = fromReferenceGeometry (R.Geometry box hit)
+{-# COMPLETE Geometry #-}
+
+-- | The reference's raw constructor (Material.hs:17): a user-defined material (README.md:11),
+-- rendered on the CPU.
+pattern Material :: (Vec3 -> HitRecord -> (Color, State StdGen R.MaterialResult)) -> Material
+pattern Material f <- (matRef -> R.Material f)
+  where Material f = fromReferenceMaterial (R.Material f)
+{-# COMPLETE Material #-}
+
+-- | The reference's raw constructor (Texture.hs:15): a user-defined texture, rendered on the CPU.
+pattern Texture :: (Point3 -> V2 Double -> Color) -> Texture
+pattern Texture f <- (texRef -> R.Texture f)
+  where Texture f = fromReferenceTexture (R.Texture f)
+{-# COMPLETE Texture #-}
+
+-- | Lift a reference value: no description, so a scene that contains it renders on the CPU
+-- through the reference's own 'R.raytrace' — by construction, whatever the closure does.
+fromReferenceGeometry :: R.Geometry m a -> Geometry m a
+fromReferenceGeometry = DeviceGeometry Nothing
+
+fromReferenceMaterial :: R.Material -> Material
+fromReferenceMaterial = DeviceMaterial Nothing
+
+fromReferenceTexture :: R.Texture -> Texture
+fromReferenceTexture = DeviceTexture Nothing
 
 -- | The reference geometry with the reference materials (what 'R.raytrace' takes).
 toReference :: Functor m => Geometry m Material -> R.Geometry m R.Material
@@ -149,23 +198,23 @@ boundingBox :: Geometry m a -> Box
 boundingBox = R.boundingBox . geoRef
 
 pureGeometry :: Applicative m => Geometry Identity a -> Geometry m a
-pureGeometry (Geometry d g) = Geometry d (R.pureGeometry g)
+pureGeometry (DeviceGeometry d g) = DeviceGeometry d (R.pureGeometry g)
 
 sphere :: Point3 -> Double -> Geometry Identity ()
-sphere c r = Geometry (Just (DSphere c r ())) (R.sphere c r)
+sphere c r = DeviceGeometry (Just (DSphere c r ())) (R.sphere c r)
 
 -- | A plane shape with a caller predicate is an arbitrary closure: CPU only.
 planeShape :: Point3 -> Vec3 -> Vec3 -> (Double -> Double -> Bool) -> (Double -> Double -> V2 Double) -> Box
            -> Geometry Identity ()
-planeShape q u v test uv bbox = Geometry Nothing (R.planeShape q u v test uv bbox)
+planeShape q u v test uv bbox = DeviceGeometry Nothing (R.planeShape q u v test uv bbox)
 
 parallelogram :: Point3 -> Vec3 -> Vec3 -> Geometry Identity ()
 parallelogram q u v =
-  Geometry (Just (DPlane 1 q u v (V2 0 0) (V2 1 0) (V2 0 1) ())) (R.parallelogram q u v)
+  DeviceGeometry (Just (DPlane 1 q u v (V2 0 0) (V2 1 0) (V2 0 1) ())) (R.parallelogram q u v)
 
 triangle :: (Point3, V2 Double) -> (Point3, V2 Double) -> (Point3, V2 Double) -> Geometry Identity ()
 triangle a@(p0, uv0) b@(p1, uv1) c@(p2, uv2) =
-  Geometry (Just (DPlane 2 p0 (p1 - p0) (p2 - p0) uv0 uv1 uv2 ())) (R.triangle a b c)
+  DeviceGeometry (Just (DPlane 2 p0 (p1 - p0) (p2 - p0) uv0 uv1 uv2 ())) (R.triangle a b c)
 
 -- | Geometry.hs:154-166: six parallelograms in the reference's order.
 cuboid :: Box -> Geometry Identity ()
@@ -176,7 +225,7 @@ cuboid box@(V3 (xmin, xmax) (ymin, ymax) (zmin, zmax)) =
       faces = [ parallelogram (V3 xmin ymin zmax) dx dy, parallelogram (V3 xmax ymin zmin) (-dx) dy
               , parallelogram (V3 xmin ymin zmin) dz dy, parallelogram (V3 xmax ymin zmax) (-dz) dy
               , parallelogram (V3 xmin ymax zmax) dx (-dz), parallelogram (V3 xmin ymin zmin) dx dz ]
-  in Geometry (DGroup <$> traverse geoDesc faces) (R.cuboid box)
+  in DeviceGeometry (DGroup <$> traverse geoDesc faces) (R.cuboid box)
 
 -- | Geometry.hs:288-294: the mesh's triangles with the reference's default texture coordinates.
 triangleMesh :: R.Mesh -> Geometry Identity ()
@@ -185,31 +234,31 @@ triangleMesh mesh@(R.Mesh verts uvs tris) =
         let uv j d = maybe d (A.index' uvs) j
         in triangle (A.index' verts i0, uv j0 (V2 0 0)) (A.index' verts i1, uv j1 (V2 1 0))
                     (A.index' verts i2, uv j2 (V2 0 1))
-  in Geometry (DGroup <$> traverse (geoDesc . tri) tris) (R.triangleMesh mesh)
+  in DeviceGeometry (DGroup <$> traverse (geoDesc . tri) tris) (R.triangleMesh mesh)
 
 constantMedium :: Double -> Geometry Identity () -> Geometry (State StdGen) ()
-constantMedium density g = Geometry ((\d -> DMedium density d ()) <$> geoDesc g) (R.constantMedium density (geoRef g))
+constantMedium density g = DeviceGeometry ((\d -> DMedium density d ()) <$> geoDesc g) (R.constantMedium density (geoRef g))
 
 group :: Monad m => [Geometry m a] -> Geometry m a
-group gs = Geometry (DGroup <$> traverse geoDesc gs) (R.group (map geoRef gs))
+group gs = DeviceGeometry (DGroup <$> traverse geoDesc gs) (R.group (map geoRef gs))
 
 bvhNode :: Monad m => Geometry m a -> Geometry m a -> Geometry m a
-bvhNode a b = Geometry (DGroup <$> traverse geoDesc [a, b]) (R.bvhNode (geoRef a) (geoRef b))
+bvhNode a b = DeviceGeometry (DGroup <$> traverse geoDesc [a, b]) (R.bvhNode (geoRef a) (geoRef b))
 
 -- | The device builds its own BVH; the closest hit (and so the image) does not depend on it.
 bvhTree :: Monad m => [Geometry m a] -> Geometry m a
-bvhTree gs = Geometry (DGroup <$> traverse geoDesc gs) (R.bvhTree (map geoRef gs))
+bvhTree gs = DeviceGeometry (DGroup <$> traverse geoDesc gs) (R.bvhTree (map geoRef gs))
 
 transform :: Functor m => M44 Double -> Geometry m a -> Geometry m a
-transform m g = Geometry (DTransform m <$> geoDesc g) (R.transform m (geoRef g))
+transform m g = DeviceGeometry (DTransform m <$> geoDesc g) (R.transform m (geoRef g))
 
 moving :: Functor m => Vec3 -> Vec3 -> Geometry m a -> Geometry m a
-moving v0 v1 g = Geometry (DMoving v0 v1 <$> geoDesc g) (R.moving v0 v1 (geoRef g))
+moving v0 v1 g = DeviceGeometry (DMoving v0 v1 <$> geoDesc g) (R.moving v0 v1 (geoRef g))
 
 -- ---------------------------------------------------------------- materials and textures
 
 mat :: Int32 -> Texture -> Double -> R.Material -> Material
-mat k t p = Material ((\d -> (k, d, p)) <$> texDesc t)
+mat k t p = DeviceMaterial ((\d -> (k, d, p)) <$> texDesc t)
 
 lightSource, lambertian, lommelSeeliger, mirror, transparent, isotropic :: Texture -> Material
 lightSource t = mat 0 t 0 (R.lightSource (texRef t))
@@ -220,41 +269,41 @@ transparent t = mat 7 t 0 (R.transparent (texRef t))
 isotropic t = mat 8 t 0 (R.isotropic (texRef t))
 
 pitchBlack :: Material
-pitchBlack = Material (Just (1, TConst (V3 0 0 0), 0)) R.pitchBlack
+pitchBlack = DeviceMaterial (Just (1, TConst (V3 0 0 0), 0)) R.pitchBlack
 
 metal :: Double -> Texture -> Material
 metal fuzz t = mat 5 t fuzz (R.metal fuzz (texRef t))
 
 dielectric :: Double -> Material
-dielectric ior = Material (Just (6, TConst (V3 0 0 0), ior)) (R.dielectric ior)
+dielectric ior = DeviceMaterial (Just (6, TConst (V3 0 0 0), ior)) (R.dielectric ior)
 
 anisotropic :: Double -> Texture -> Material
 anisotropic g t = mat 9 t g (R.anisotropic g (texRef t))
 
 constantTexture :: Color -> Texture
-constantTexture c = Texture (Just (TConst c)) (R.constantTexture c)
+constantTexture c = DeviceTexture (Just (TConst c)) (R.constantTexture c)
 
 solidTexture :: (Point3 -> Color) -> Texture
-solidTexture f = Texture Nothing (R.solidTexture f)
+solidTexture f = DeviceTexture Nothing (R.solidTexture f)
 
 uvTexture :: (V2 Double -> Color) -> Texture
-uvTexture f = Texture Nothing (R.uvTexture f)
+uvTexture f = DeviceTexture Nothing (R.uvTexture f)
 
 imageTexture :: A.Manifest r Color => A.Matrix r Color -> Texture
 imageTexture img =
   let A.Sz (h A.:. w) = A.size img
       texels = A.toList img
       fingerprint = sum (zipWith (\k (V3 r g b) -> fromIntegral (k + 1) * (r + 3 * g + 7 * b)) [0 :: Int ..] texels)
-  in Texture (Just (TImage w h fingerprint texels)) (R.imageTexture img)
+  in DeviceTexture (Just (TImage w h fingerprint texels)) (R.imageTexture img)
 
 checkerTexture :: Int -> Int -> Color -> Color -> Texture
-checkerTexture nu nv c0 c1 = Texture (Just (TChecker nu nv c0 c1)) (R.checkerTexture nu nv c0 c1)
+checkerTexture nu nv c0 c1 = DeviceTexture (Just (TChecker nu nv c0 c1)) (R.checkerTexture nu nv c0 c1)
 
 noiseTexture :: Int -> Double -> V3 Double -> Color -> Color -> Texture
-noiseTexture k f s c0 c1 = Texture (Just (TNoise k f s c0 c1)) (R.noiseTexture k f s c0 c1)
+noiseTexture k f s c0 c1 = DeviceTexture (Just (TNoise k f s c0 c1)) (R.noiseTexture k f s c0 c1)
 
 marbleTexture :: Vec3 -> Double -> V3 Double -> Texture
-marbleTexture d f s = Texture (Just (TMarble d f s)) (R.marbleTexture d f s)
+marbleTexture d f s = DeviceTexture (Just (TMarble d f s)) (R.marbleTexture d f s)
 
 -- ===================================================================== flattening
 -- raytrace_amd/scene.py:flatten, restated: rigid transforms and motion baked into the leaves,
@@ -275,9 +324,69 @@ data Flat = Flat
   , fTexs :: [TexD]                         -- reversed
   , fMotions :: [(Vec3, Vec3)]              -- reversed
   , fFrames :: Map.Map [Double] Int32
-  , fGids :: Map.Map (Int32, [Double], Maybe (Vec3, Vec3)) Int32
+  , fGids :: Map.Map (Int32, [Double], Maybe (Vec3, Vec3), Int32) Int32
   , fOrder :: Int32
+  , fBlas :: Map.Map Int (Int32, Int32)     -- shared object (tagShared key) -> (object index, leaves)
+  , fInstances :: [(Int32, Int32, M34)]     -- (object, depth-first order of its first leaf, placement), reversed
   }
+
+-- | rt.h RT_SET_BLAS: the set of an instanced object's object-space leaves.
+setBlas :: Int32 -> Int32
+setBlas b = -1 - b
+
+-- | A rigid `transform` over at least this many leaves is a two-level instance (rt_instance), not
+-- baked (raytrace_amd/scene.py INSTANCE_MIN_LEAVES; smaller objects are cheaper to trace baked).
+instanceMinLeaves :: Int
+instanceMinLeaves = 64
+
+leafCount :: Desc a -> Int
+leafCount d = case d of
+  DSphere{} -> 1
+  DPlane{} -> 1
+  DGroup cs -> sum (map leafCount cs)
+  DTransform _ c -> leafCount c
+  DPlaced _ _ c -> leafCount c
+  DMoving _ _ c -> leafCount c
+  DMedium _ b _ -> leafCount b
+
+-- | Subtrees with `moving` or media stay baked (an instance has one rigid placement).
+bakesOnly :: Desc a -> Bool
+bakesOnly d = case d of
+  DMoving{} -> True
+  DMedium{} -> True
+  DGroup cs -> any bakesOnly cs
+  DTransform _ c -> bakesOnly c
+  DPlaced _ _ c -> bakesOnly c
+  _ -> False
+
+-- | Tag every `transform`'s child with the identity of its VALUE (a StableName): the placements
+-- of one shared object, e.g. @map (\m -> transform m bunny) placements@, get the same key and
+-- share one object-space BVH (rt_instance), as raytrace_amd/scene.py does with object identity.
+-- Children that are equal but separately built get separate keys: correct, only less shared.
+tagShared :: forall a. Desc a -> IO (Desc a)
+tagShared root = do
+  table <- newIORef (Map.empty :: Map.Map Int [(StableName (Desc a), Int)])
+  next <- newIORef (0 :: Int)
+  let keyOf :: Desc a -> IO Int
+      keyOf c = do
+        sn <- makeStableName $! c
+        bucket <- Map.findWithDefault [] (hashStableName sn) <$> readIORef table
+        case [ k | (o, k) <- bucket, eqStableName o sn ] of
+          (k : _) -> pure k
+          [] -> do
+            k <- readIORef next
+            writeIORef next (k + 1)
+            modifyIORef' table (Map.insert (hashStableName sn) ((sn, k) : bucket))
+            pure k
+      go :: Desc a -> IO (Desc a)
+      go d = case d of
+        DGroup cs -> DGroup <$> mapM go cs
+        DTransform m c -> do
+          k <- keyOf c
+          DPlaced k m <$> go c
+        DMoving v0 v1 c -> DMoving v0 v1 <$> go c
+        _ -> pure d  -- leaves; a medium's boundary is always baked (its set is not 0)
+  go root
 
 -- | 3 x 4 affine part of a 4 x 4 matrix, row-major.
 type M34 = [[Double]]
@@ -313,7 +422,7 @@ v2l (V2 x y) = [x, y]
 flatten :: Desc Material -> Maybe Flat
 flatten root = execStateM (walk root Nothing Nothing 0) empty
   where
-    empty = Flat [] [] Map.empty [] Map.empty [] [] Map.empty Map.empty 0
+    empty = Flat [] [] Map.empty [] Map.empty [] [] Map.empty Map.empty 0 Map.empty []
     execStateM m s = case m s of
       Nothing -> Nothing
       Just ((), s') -> Just s'
@@ -330,6 +439,23 @@ walk node m34 mv set = case node of
     let m3 = m34Of m
     in if not (rigid m3) then const Nothing
        else walk c (Just (maybe m3 (`compose` m3) m34)) mv set
+  DPlaced key m c ->
+    let m3 = m34Of m
+        m2 = maybe m3 (`compose` m3) m34
+    in if not (rigid m3) then const Nothing
+       else if set /= 0 || mv /= Nothing || leafCount c < instanceMinLeaves || bakesOnly c
+         then walk c (Just m2) mv set
+         else \s0 -> do
+           -- two-level instancing (rt_instance): the object's leaves once, in object space, in set
+           -- RT_SET_BLAS(b) with orders 0 .. n-1; each placement takes the next n orders
+           (b, n, s1) <- case Map.lookup key (fBlas s0) of
+             Just (b, n) -> Just (b, n, s0)
+             Nothing -> do
+               let b = fromIntegral (Map.size (fBlas s0))
+               ((), sObj) <- walk c Nothing Nothing (setBlas b) s0 { fOrder = 0 }
+               let n = fOrder sObj
+               Just (b, n, sObj { fOrder = fOrder s0, fBlas = Map.insert key (b, n) (fBlas sObj) })
+           Just ((), s1 { fInstances = (b, fOrder s1, m2) : fInstances s1, fOrder = fOrder s1 + n })
   DMoving v0 v1 c ->
     let rot v = maybe v (`mulVector` v) m34
         (w0, w1) = (rot v0, rot v1)
@@ -365,12 +491,12 @@ walk node m34 mv set = case node of
              Just i -> Just (i, s)
              Nothing -> let i = fromIntegral (Map.size (fFrames s)) in Just (i, s { fFrames = Map.insert rt i (fFrames s) })
     leaf m body s0 = do
-      (mi, s1) <- if set == 0 then materialIndex m s0 else Just (-1, s0)
+      (mi, s1) <- if set <= 0 then materialIndex m s0 else Just (-1, s0)
       ((kind, p, uv, uvf), s2) <- body s1
       let (mo, s3) = case mv of
             Nothing -> (-1, s2)
             Just pair -> (fromIntegral (length (fMotions s2)), s2 { fMotions = pair : fMotions s2 })
-          key = (kind, p, mv)
+          key = (kind, p, mv, min 0 set)  -- an instanced object's leaves: a gid space of their own
           (gid, s4) = case Map.lookup key (fGids s3) of
             Just g -> (g, s3)
             Nothing -> let g = fromIntegral (Map.size (fGids s3)) in (g, s3 { fGids = Map.insert key g (fGids s3) })
@@ -384,8 +510,8 @@ seqAll (f : fs) s = f s >>= \((), s') -> seqAll fs s'
 -- | The table index of a material (and of its texture), shared by every leaf that uses the same
 -- (kind, parameter, texture); Nothing for a closure texture.
 materialIndex :: Material -> FM Int32
-materialIndex (Material Nothing _) _ = Nothing
-materialIndex (Material (Just (kind, tex, param)) _) s0 =
+materialIndex (DeviceMaterial Nothing _) _ = Nothing
+materialIndex (DeviceMaterial (Just (kind, tex, param)) _) s0 =
   let tk = texKey tex
       (ti, s1) = case Map.lookup tk (fTexIx s0) of
         Just i -> (i, s0)
@@ -474,7 +600,9 @@ withFlatScene Flat{..} k =
       images = [ cs | TImage _ _ _ cs <- texs ]
       texels = concat images
       needPerlin = or [ True | TNoise{} <- texs ] || or [ True | TMarble{} <- texs ]
+      insts = reverse fInstances
   in allocaBytes (max 1 (152 * length prims)) $ \pp ->
+     allocaBytes (max 1 (112 * length insts)) $ \pin ->
      allocaBytes (max 1 (16 * length media)) $ \pm ->
      allocaBytes (max 1 (16 * length mats)) $ \pmat ->
      allocaBytes (max 1 (128 * nTex)) $ \pt ->
@@ -518,13 +646,18 @@ withFlatScene Flat{..} k =
        forM_ (zip [0 ..] texels) $ \(i, V3 r g bl) ->
          zipWithM_ (\c x -> pokeByteOff ptx (12 * i + 4 * c) (realToFrac x :: CFloat)) [0 ..] [r, g, bl]
        when needPerlin $ do
-         -- Noise.hs:52-92: the reference's own tables — permX / permY / permZ, and the gradients
-         -- exactly as Noise.hs:88-92 computes them (randomUnitVector under mkStdGen 666)
-         forM_ (zip [0 :: Int ..] [permX, permY, permZ]) $ \(a, perm) ->
-           forM_ [0 .. 255] $ \j -> pokeI32 pper (4 * (256 * a + j)) (fromIntegral (A.index' perm j))
+         -- Noise.hs:52-92: the reference's permutation tables (embedded below: Graphics.Ray.Noise
+         -- does not export them) and the gradients exactly as Noise.hs:88-92 computes them
+         -- (randomUnitVector under mkStdGen 666)
+         forM_ (zip [0 :: Int ..] [permXTable, permYTable, permZTable]) $ \(a, perm) ->
+           zipWithM_ (\j v -> pokeI32 pper (4 * (256 * a + j)) (fromIntegral v)) [0 .. 255] perm
          let grads = evalState (mapM (const randomUnitVector) [1 .. 256 :: Int]) (mkStdGen 666) :: [V3 Double]
          forM_ (zip [0 ..] grads) $ \(j, g) -> pokeDoubles pper (3072 + 24 * j) (v3l g)
-       fillBytes sc 0 136  -- n_instances = 0: this flatten bakes every transform into world space
+       forM_ (zip [0 ..] insts) $ \(i, (b, o, m)) -> do
+         let q = pin `plusPtr` (112 * i)
+         pokeI32 q 0 b >> pokeI32 q 4 (-1) >> pokeI32 q 8 o >> pokeI32 q 12 0  -- material -1: the leaves' own
+         pokeDoubles q 16 (concat m)
+       fillBytes sc 0 136
        let arr off n p = pokeI32 sc off (fromIntegral n) >> pokeByteOff sc (off + 8) (if n > 0 then castPtr p else nullPtr :: Ptr ())
        arr 0 (length prims) pp
        arr 16 (length media) pm
@@ -534,7 +667,55 @@ withFlatScene Flat{..} k =
        arr 80 (length frames) pf
        arr 96 (length texels) ptx
        pokeByteOff sc 112 (if needPerlin then castPtr pper else nullPtr :: Ptr ())
+       arr 120 (length insts) pin
        k (castPtr sc)
+
+-- Noise.hs:52-86 permX / permY / permZ (raytrace_amd/data/perlin_perm.json; the constants of the
+-- reference's module, embedded so that the binding asks no change of it)
+permXTable :: [Int]
+permXTable =
+  [ 179, 60, 35, 16, 220, 94, 67, 236, 106, 112, 65, 166, 83, 101, 246, 140, 219, 186, 113, 88, 153, 70, 34, 63
+  , 157, 210, 212, 188, 54, 74, 23, 161, 28, 137, 126, 107, 183, 58, 134, 127, 211, 225, 17, 123, 150, 243, 160, 68
+  , 75, 239, 173, 221, 89, 109, 61, 72, 159, 80, 154, 18, 214, 144, 197, 24, 105, 32, 84, 226, 136, 29, 139, 97
+  , 230, 167, 165, 238, 27, 14, 50, 193, 46, 253, 240, 111, 69, 196, 130, 102, 104, 118, 204, 12, 169, 202, 142, 25
+  , 245, 215, 149, 138, 185, 48, 223, 247, 47, 98, 143, 26, 87, 251, 103, 52, 234, 232, 218, 205, 92, 228, 162, 85
+  , 122, 191, 242, 164, 129, 192, 255, 231, 147, 91, 178, 213, 176, 36, 120, 155, 241, 222, 177, 20, 152, 141, 51, 171
+  , 250, 95, 71, 119, 254, 172, 53, 146, 135, 124, 125, 163, 235, 99, 7, 22, 100, 229, 93, 174, 3, 189, 116, 66
+  , 217, 158, 237, 55, 151, 0, 148, 45, 86, 64, 216, 43, 252, 121, 200, 115, 39, 184, 82, 56, 9, 181, 62, 2
+  , 81, 209, 44, 79, 19, 110, 41, 10, 194, 15, 132, 224, 249, 96, 233, 117, 49, 203, 5, 37, 11, 59, 168, 114
+  , 90, 131, 31, 145, 40, 206, 13, 187, 133, 207, 4, 199, 170, 78, 30, 182, 248, 21, 6, 227, 57, 180, 73, 42
+  , 128, 175, 108, 33, 244, 201, 198, 77, 195, 8, 38, 190, 76, 156, 208, 1
+  ]
+
+permYTable :: [Int]
+permYTable =
+  [ 252, 123, 131, 151, 243, 143, 12, 247, 196, 179, 99, 0, 178, 109, 71, 160, 93, 205, 127, 38, 142, 117, 152, 124
+  , 166, 95, 200, 121, 15, 17, 10, 190, 116, 158, 173, 75, 248, 191, 197, 58, 70, 184, 226, 146, 6, 239, 165, 113
+  , 218, 34, 83, 77, 74, 5, 176, 85, 112, 147, 59, 66, 14, 31, 2, 21, 198, 108, 255, 11, 36, 156, 96, 73
+  , 1, 189, 126, 50, 220, 16, 249, 23, 139, 135, 141, 92, 159, 4, 119, 174, 171, 253, 86, 227, 251, 172, 7, 149
+  , 207, 212, 224, 44, 187, 91, 175, 84, 28, 211, 180, 195, 52, 98, 244, 125, 138, 54, 210, 201, 209, 219, 133, 240
+  , 9, 202, 199, 42, 51, 48, 104, 154, 88, 53, 64, 105, 242, 63, 223, 222, 67, 238, 32, 134, 72, 62, 101, 150
+  , 94, 161, 19, 236, 215, 97, 206, 22, 188, 230, 170, 18, 13, 162, 129, 90, 246, 130, 35, 46, 43, 213, 29, 76
+  , 241, 61, 30, 136, 235, 87, 114, 68, 183, 177, 250, 132, 3, 122, 110, 145, 81, 78, 232, 69, 60, 80, 216, 65
+  , 164, 237, 157, 203, 25, 221, 254, 181, 8, 182, 214, 24, 40, 102, 37, 106, 228, 39, 229, 163, 111, 186, 245, 55
+  , 41, 225, 234, 49, 45, 231, 107, 103, 168, 153, 47, 56, 118, 120, 137, 155, 148, 82, 33, 204, 79, 169, 144, 20
+  , 27, 128, 192, 217, 100, 208, 115, 140, 233, 89, 193, 185, 167, 57, 26, 194
+  ]
+
+permZTable :: [Int]
+permZTable =
+  [ 153, 90, 163, 138, 20, 136, 79, 100, 93, 38, 185, 31, 193, 43, 161, 2, 30, 37, 87, 6, 127, 207, 96, 51
+  , 27, 227, 203, 215, 155, 190, 106, 94, 65, 183, 114, 71, 74, 219, 245, 39, 140, 216, 195, 191, 3, 214, 13, 23
+  , 168, 179, 218, 133, 102, 53, 194, 124, 166, 108, 116, 246, 35, 109, 220, 121, 205, 110, 83, 242, 252, 231, 25, 128
+  , 61, 57, 187, 222, 189, 228, 148, 101, 239, 162, 48, 150, 55, 174, 178, 42, 200, 160, 58, 206, 11, 92, 204, 67
+  , 8, 113, 34, 172, 181, 177, 66, 16, 243, 159, 197, 135, 249, 241, 28, 147, 158, 139, 176, 88, 29, 149, 254, 226
+  , 192, 201, 202, 186, 69, 45, 72, 199, 107, 99, 209, 10, 230, 217, 247, 89, 50, 129, 15, 64, 248, 167, 180, 146
+  , 210, 169, 4, 81, 97, 238, 5, 237, 125, 236, 95, 9, 104, 221, 32, 86, 165, 134, 224, 182, 198, 234, 253, 59
+  , 164, 52, 60, 208, 103, 22, 46, 188, 54, 12, 1, 112, 144, 137, 47, 156, 98, 78, 18, 82, 175, 225, 19, 184
+  , 244, 49, 120, 157, 130, 70, 80, 251, 212, 250, 119, 118, 196, 223, 105, 68, 84, 21, 145, 173, 56, 235, 91, 17
+  , 126, 76, 131, 117, 152, 111, 33, 36, 233, 141, 122, 85, 7, 123, 44, 62, 115, 26, 0, 40, 229, 211, 213, 63
+  , 143, 77, 14, 24, 142, 154, 73, 132, 171, 41, 170, 240, 75, 151, 232, 255
+  ]
 
 -- | cs_background restricted to what the device evaluates: (1 - a) c0 + a c1 with
 -- a = (y + 1) / 2 (`const c` is c0 = c1; test/Main.hs's `sky` and `grayFade`).  The closure is
@@ -588,12 +769,17 @@ data RenderError
   | LibraryError Int String       -- ^ an RT_E_* code and rt_last_error's message
   deriving (Show)
 
+-- | The 8-bit transfer of the reference's writers: 'SRGB' = writeImage, 'Sqrt' = writeImageSqrt
+-- (Ray.hs:248-260); rt.h RT_EXEC_ENCODE8_SRGB / RT_EXEC_ENCODE8_SQRT.
+data Encoding = SRGB | Sqrt
+  deriving (Eq, Show)
+
 -- | Number of visible HIP devices (0 when there is none).
 deviceCount :: IO Int
 deviceCount = (\n -> if n > 0 then fromIntegral n else 0) <$> c_rt_device_count
 
-withExec :: DeviceOptions -> [Int] -> (Ptr RtExec -> IO a) -> IO a
-withExec DeviceOptions{..} devs k =
+withExec :: DeviceOptions -> Maybe Encoding -> [Int] -> (Ptr RtExec -> IO a) -> IO a
+withExec DeviceOptions{..} enc devs k =
   withArray (map fromIntegral devs :: [Int32]) $ \pd ->
   allocaBytes 32 $ \p -> do
     fillBytes p 0 32
@@ -601,7 +787,9 @@ withExec DeviceOptions{..} devs k =
     pokeI32 p 4 1                                              -- n_shards: the whole image
     pokeI32 p 8 0
     pokeI32 p 12 (fromIntegral (max 1 doRowBlock))
-    pokeI32 p 16 (if doPrecision == Float32 then 1 else 0)     -- RT_EXEC_F32
+    let flags = (if doPrecision == Float32 then 1 else 0)     -- RT_EXEC_F32
+              + (case enc of Nothing -> 0; Just SRGB -> 2; Just Sqrt -> 4)  -- RT_EXEC_ENCODE8_*
+    pokeI32 p 16 flags
     pokeI32 p 20 (fromIntegral (length devs))
     pokeByteOff p 24 (castPtr pd :: Ptr ())
     k (castPtr p)
@@ -615,42 +803,95 @@ philoxKey g = let (seed, gamma) = unseedSMGen (unStdGen g) in mix64 (seed `xor` 
                    z2 = (z1 `xor` (z1 `shiftR` 33)) * 0xc4ceb9fe1a85ec53
                in z2 `xor` (z2 `shiftR` 33)
 
+-- | One rt_render call into a fresh ForeignPtr of h x w elements of 3 `elem`s each: the scene
+-- flattened (shared transformed objects instanced), the camera reified, the device list resolved.
+renderRaw :: Storable e => DeviceOptions -> Maybe Encoding -> R.CameraSettings -> Geometry m Material -> StdGen
+          -> (Int -> IO (ForeignPtr e)) -> IO (Either RenderError (Int, Int, ForeignPtr e))
+renderRaw opts enc settings world gen alloc =
+  case (geoDesc world, reifyBackground (R.cs_background settings)) of
+    (Just desc, Just bg) -> do
+      tagged <- tagShared desc
+      case flatten tagged of
+        Nothing -> pure (Left NotReifiable)
+        Just flat -> do
+          devs <- case doDevices opts of
+            Just ds -> pure ds
+            Nothing -> (\n -> [0 .. max 1 n - 1]) <$> deviceCount
+          withCamera settings bg $ \cam ->
+            withFlatScene flat $ \sc ->
+            withExec opts enc devs $ \ex -> do
+              h <- fromIntegral <$> c_rt_image_height cam
+              let w = R.cs_imageWidth settings
+              if h <= 0 || w <= 0 then pure (Left (LibraryError (-2) "empty image")) else do
+                fp <- alloc (3 * h * w)
+                rc <- withForeignPtr fp $ \out -> c_rt_render cam sc (philoxKey gen) ex (castPtr out) nullPtr
+                if rc /= 0
+                  then Left . LibraryError (fromIntegral rc) <$> (c_rt_last_error >>= peekCString)
+                  else pure (Right (h, w, fp))
+    _ -> pure (Left NotReifiable)
+
 -- | Render on the GPU through rt_render.  The output buffer is a ForeignPtr that becomes the
--- storable (S) massiv matrix directly: no copy, no list.
+-- storable (S) massiv matrix directly: no copy, no list (binary64); the FP32 path widens the
+-- floats in one pass over the buffer.
 renderOnDevice :: DeviceOptions -> R.CameraSettings -> Geometry m Material -> StdGen
                -> IO (Either RenderError (A.Matrix A.S Color))
-renderOnDevice opts settings world gen =
-  case (geoDesc world >>= flatten, reifyBackground (R.cs_background settings)) of
-    (Just flat, Just bg) -> do
-      devs <- case doDevices opts of
-        Just ds -> pure ds
-        Nothing -> (\n -> [0 .. max 1 n - 1]) <$> deviceCount
-      withCamera settings bg $ \cam ->
-        withFlatScene flat $ \sc ->
-        withExec opts devs $ \ex -> do
-          h <- fromIntegral <$> c_rt_image_height cam
-          let w = R.cs_imageWidth settings
-              n = h * w
-          if h <= 0 || w <= 0 then pure (Left (LibraryError (-2) "empty image")) else do
-            fp <- mallocForeignPtrArray n :: IO (ForeignPtr Color)   -- V3 Double = 3 contiguous doubles
-            rc <- withForeignPtr fp $ \out ->
-              if doPrecision opts == Binary64
-                then c_rt_render cam sc (philoxKey gen) ex (castPtr out) nullPtr
-                else allocaArray (3 * n) $ \tmp -> do
-                  r <- c_rt_render cam sc (philoxKey gen) ex (castPtr (tmp :: Ptr CFloat)) nullPtr
-                  when (r == 0) $ forM_ [0 .. n - 1] $ \i -> do
-                    [x, y, z] <- mapM (\c -> realToFrac <$> peekElemOff tmp (3 * i + c)) [0, 1, 2]
-                    pokeElemOff out i (V3 x y z)
-                  pure r
-            if rc /= 0
-              then Left . LibraryError (fromIntegral rc) <$> (c_rt_last_error >>= peekCString)
-              else pure (Right (A.resize' (A.Sz2 h w) (AU.unsafeArrayFromForeignPtr0 A.Par fp (A.Sz1 n))))
-    _ -> pure (Left NotReifiable)
+renderOnDevice opts settings world gen
+  | doPrecision opts == Binary64 = do
+      r <- renderRaw opts Nothing settings world gen (\n -> mallocForeignPtrArray n :: IO (ForeignPtr CDouble))
+      pure (fmap (\(h, w, fp) -> asColors h w (castForeignPtr fp)) r)
+  | otherwise = do
+      r <- renderRaw opts Nothing settings world gen (\n -> mallocForeignPtrArray n :: IO (ForeignPtr CFloat))
+      case r of
+        Left e -> pure (Left e)
+        Right (h, w, fp32) -> do
+          let n = 3 * h * w
+          fp <- mallocForeignPtrArray n :: IO (ForeignPtr CDouble)
+          withForeignPtr fp32 $ \src -> withForeignPtr fp $ \dst ->
+            forM_ [0 .. n - 1] $ \i -> peekElemOff src i >>= pokeElemOff dst i . realToFrac
+          pure (Right (asColors h w (castForeignPtr fp)))
+  where
+    -- V3 Double is stored as 3 contiguous doubles (linear's Storable instance)
+    asColors h w fp = A.resize' (A.Sz2 h w) (AU.unsafeArrayFromForeignPtr0 A.Par (fp :: ForeignPtr Color) (A.Sz1 (h * w)))
+
+-- | The 8-bit codes writeImage / writeImageSqrt would store for the render, encoded on the GPU
+-- right after the gather (rt.h RT_EXEC_ENCODE8_*): h x w (R, G, B) bytes, bit-identical to
+-- encoding the linear render.
+renderImage8 :: DeviceOptions -> Encoding -> R.CameraSettings -> Geometry m Material -> StdGen
+             -> IO (Either RenderError (A.Matrix A.S (V3 Word8)))
+renderImage8 opts enc settings world gen = do
+  r <- renderRaw opts (Just enc) settings world gen (\n -> mallocForeignPtrBytes n :: IO (ForeignPtr Word8))
+  pure (fmap (\(h, w, fp) -> A.resize' (A.Sz2 h w)
+                (AU.unsafeArrayFromForeignPtr0 A.Par (castForeignPtr fp :: ForeignPtr (V3 Word8)) (A.Sz1 (h * w)))) r)
+
+-- | Render and write the image file in one step: @raytraceToFile SRGB path cs world gen@ writes
+-- what @writeImage path (raytrace cs world gen)@ writes (Sqrt: writeImageSqrt), with the 8-bit
+-- encoding done on the GPU; scenes the device cannot render go through the reference's CPU
+-- raytrace and writer.
+raytraceToFile :: (R.ToRandom m, Functor m) => Encoding -> FilePath -> R.CameraSettings -> Geometry m Material
+               -> StdGen -> IO ()
+raytraceToFile enc path settings world gen = do
+  r <- renderImage8 defaultDeviceOptions enc settings world gen
+  case r of
+    Right codes -> I.writeImageAuto path (A.map toPixel codes)
+    Left e | fallback e -> (if enc == SRGB then R.writeImage else R.writeImageSqrt) path
+                             (R.raytrace settings (toReference world) gen)
+           | otherwise -> ioError (userError ("Graphics.Ray.Device.raytraceToFile: " ++ show e))
+  where
+    -- the codes are already the stored 8-bit values: written as non-linear sRGB bytes, unconverted
+    toPixel :: V3 Word8 -> C.Pixel (SRGB 'NonLinear) Word8
+    toPixel (V3 r g b) = C.Pixel (C.ColorSRGB r g b)
+
+-- | Library results that send a render to the reference's CPU path: a closure somewhere in the
+-- scene, RT_E_UNSUPPORTED (e.g. a non-Euclidean transform) and RT_E_STACK (a hierarchy deeper
+-- than the device's traversal stack).
+fallback :: RenderError -> Bool
+fallback NotReifiable = True
+fallback (LibraryError code _) = code == -3 || code == -5
 
 -- | 'Graphics.Ray.raytrace' on the GPU: same arguments, same result (Ray.hs:121-238).  Falls
 -- back to the reference's CPU path when the scene is not reifiable or the library reports
--- RT_E_UNSUPPORTED; any other library error (no device, a HIP failure) is raised.  The
--- constraint adds `Functor m` to the reference's `ToRandom m` (the CPU fallback maps the
+-- RT_E_UNSUPPORTED or RT_E_STACK; any other library error (no device, a HIP failure) is raised.
+-- The constraint adds `Functor m` to the reference's `ToRandom m` (the CPU fallback maps the
 -- reference materials over the geometry); every geometry monad (Identity, State StdGen) is one.
 raytrace :: (R.ToRandom m, Functor m) => R.CameraSettings -> Geometry m Material -> StdGen -> A.Matrix A.D Color
 raytrace = raytraceWith defaultDeviceOptions
@@ -660,9 +901,6 @@ raytraceWith :: (R.ToRandom m, Functor m) => DeviceOptions -> R.CameraSettings -
 raytraceWith opts settings world gen =
   case unsafePerformIO (renderOnDevice opts settings world gen) of
     Right img -> A.delay img
-    Left NotReifiable -> cpu
-    Left (LibraryError (-3) _) -> cpu                        -- RT_E_UNSUPPORTED
-    Left (LibraryError code msg) -> error ("Graphics.Ray.Device.raytrace: rt_render failed (" ++ show code ++ "): " ++ msg)
-  where
-    cpu = R.raytrace settings (toReference world) gen
+    Left e | fallback e -> R.raytrace settings (toReference world) gen
+           | otherwise -> error ("Graphics.Ray.Device.raytrace: rt_render failed: " ++ show e)
 {-# NOINLINE raytraceWith #-}

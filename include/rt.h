@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 /* status codes */
 #define RT_OK 0
@@ -190,6 +190,13 @@ typedef struct rt_camera_settings {
 
 /* rt_exec.flags */
 #define RT_EXEC_F32 1          /* FP32 kernel, float output (default: binary64, double output) */
+/* 8-bit output (rt_render / rt_multi_render only): out_rgb receives uint8 codes, one per channel,
+   exactly what writeImage (sRGB) / writeImageSqrt (sqrt) store (Ray.hs:248-260):
+   min(255, floor(256 * transfer(clamp01 x))) of the linear mean, NaN -> 0 — the fused epilogue
+   of rt_encode8_async, run on the gathering device after the gather.  Bit-identical to encoding
+   the linear render on the host. */
+#define RT_EXEC_ENCODE8_SRGB 2
+#define RT_EXEC_ENCODE8_SQRT 4
 
 #define RT_MAX_DEVICES 64
 
@@ -203,10 +210,12 @@ typedef struct rt_camera_settings {
  *
  * Device list (rt_render only; one process, many GPUs).  With n_devices >= 1 and n_shards == 1
  * the call renders the WHOLE image over devices[0 .. n_devices-1]: device k renders shard k of
- * n_devices (same row interleave), all devices concurrently on their own streams, and the
- * shard tiles are gathered into out_rgb (each device copies its tile to the host; the host
- * un-permutes the rows).  A device may appear more than once (two shards on one GPU).  The
- * image is bit-identical to the single-device render.  n_devices == 0: `device` alone. */
+ * n_devices (same row interleave), all devices concurrently on their own streams.  The scene is
+ * built on the host ONCE and uploaded to the distinct devices concurrently; each device copies its
+ * tile into devices[0]'s framebuffer (peer-to-peer over xGMI, the rows un-permuted by the copy's
+ * stride), and one device-to-host copy fills out_rgb.  A device may appear more than once (two
+ * shards on one GPU).  The image is bit-identical to the single-device render.  n_devices == 0:
+ * `device` alone.  rt_multi_scene_create keeps such a scene resident across renders. */
 typedef struct rt_exec {
   int32_t device;       /* HIP device ordinal (n_devices == 0) */
   int32_t n_shards;     /* >= 1 */
@@ -227,6 +236,7 @@ typedef struct rt_stats {
 } rt_stats;
 
 typedef struct rt_device_scene rt_device_scene;   /* opaque, device-resident scene */
+typedef struct rt_multi_scene rt_multi_scene;     /* opaque, resident on a list of devices */
 
 int rt_abi_version(void);
 const char* rt_last_error(void);   /* thread-local message of the last failing call */
@@ -243,12 +253,14 @@ int rt_shard_row(int32_t t, const rt_exec* ex);
 
 /* One-shot host-buffer call — the Haskell binding's entry point (replaces Ray.hs:121-238).
  * out_rgb: caller-owned host buffer of rt_shard_rows(h, ex) * image_width * 3 doubles (floats
- * with RT_EXEC_F32); the whole image when n_shards == 1.  Returns RT_OK or a negative RT_E_*
+ * with RT_EXEC_F32, uint8 codes with RT_EXEC_ENCODE8_*); the whole image when n_shards == 1.  Returns RT_OK or a negative RT_E_*
  * code. */
 int rt_render(const rt_camera_settings* cs, const rt_scene* scene, uint64_t seed, const rt_exec* ex,
               void* out_rgb, rt_stats* stats);
 
-/* Device-resident path (used when inputs already live in HBM, e.g. bench.py / torch callers). */
+/* Device-resident path (used when inputs already live in HBM, e.g. bench.py / torch callers).
+ * The scene is built on the host at create; a precision's records are uploaded on its first
+ * render (rt_stats.upload_ms of rt_scene_stats covers what has been uploaded so far). */
 int rt_scene_create(const rt_scene* scene, int32_t device, rt_device_scene** out);
 int rt_scene_destroy(rt_device_scene* s);
 int rt_scene_stats(const rt_device_scene* s, rt_stats* stats);
@@ -258,6 +270,17 @@ int rt_scene_stats(const rt_device_scene* s, rt_stats* stats);
  * the work. */
 int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex,
                     void* d_out_rgb, void* hip_stream);
+
+/* Multi-device resident scene (one process, many GPUs; what a caller that renders the same scene
+ * more than once keeps between rt_render-like calls): one host build, concurrent uploads to the
+ * distinct devices of the list.  rt_multi_render renders as rt_render does with this device list
+ * (ex->n_devices must be 0; ex->n_shards 1, row_block and flags as in rt_render) into the
+ * caller's host buffer out_rgb (h * width * 3 doubles, floats with RT_EXEC_F32, bytes with
+ * RT_EXEC_ENCODE8_*).  A list of one device also renders an rt_exec shard (n_shards > 1). */
+int rt_multi_scene_create(const rt_scene* scene, const int32_t* devices, int32_t n_devices, rt_multi_scene** out);
+int rt_multi_scene_destroy(rt_multi_scene* m);
+int rt_multi_render(const rt_multi_scene* m, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex,
+                    void* out_rgb, rt_stats* stats);
 
 /* Fused output epilogue of writeImage / writeImageSqrt (Ray.hs:248-260): linear RGB (float, or
  * double with in_f64 = 1) -> 8-bit codes min(255, floor(256 * transfer(clamp01 x))), transfer =

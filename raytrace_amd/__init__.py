@@ -16,7 +16,7 @@ from .geometry import (M44, Mesh, ObjParseError, boundingBox, bvhNode, bvhTree, 
 from .material import (Material, Texture, anisotropic, checkerTexture, constantTexture, dielectric, imageTexture,
                        isotropic, lambertian, lightSource, lommelSeeliger, marbleTexture, metal, mirror, noiseTexture,
                        pitchBlack, solidTexture, transparent, uvTexture)
-from .ray import DeviceScene, encode8, raytrace, readImage, render_shard, writeImage, writeImageSqrt
+from .ray import DeviceScene, MultiDeviceScene, encode8, raytrace, readImage, render_shard, writeImage, writeImageSqrt
 from .scene import FlatScene, flatten
 
 __version__ = "0.1.0"

@@ -15,7 +15,8 @@ LIB_PATH = os.environ.get("RT_AMD_LIB") or os.path.join(HERE, "_lib", "librt_amd
 RT_OK, RT_E_GENERIC, RT_E_INVALID, RT_E_UNSUPPORTED, RT_E_HIP, RT_E_STACK = 0, -1, -2, -3, -4, -5
 
 EXPORTED = ["rt_abi_version", "rt_last_error", "rt_device_count", "rt_image_height", "rt_shard_rows", "rt_shard_row", "rt_render",
-            "rt_scene_create", "rt_scene_destroy", "rt_scene_stats", "rt_render_async", "rt_encode8_async"]
+            "rt_scene_create", "rt_scene_destroy", "rt_scene_stats", "rt_render_async", "rt_encode8_async",
+            "rt_multi_scene_create", "rt_multi_scene_destroy", "rt_multi_render"]
 
 
 class RtRedirectTarget(ctypes.Structure):
@@ -51,7 +52,10 @@ class RtScene(ctypes.Structure):
 
 
 RT_EXEC_F32 = 1  # rt_exec.flags: FP32 kernel, float output (default: binary64, double output)
-ABI_VERSION = 3
+RT_EXEC_ENCODE8_SRGB = 2  # rt_render output: uint8 codes of writeImage (sRGB)
+RT_EXEC_ENCODE8_SQRT = 4  # rt_render output: uint8 codes of writeImageSqrt
+ENCODINGS = {None: 0, "srgb": RT_EXEC_ENCODE8_SRGB, "sqrt": RT_EXEC_ENCODE8_SQRT}
+ABI_VERSION = 4
 PRECISIONS = {"f64": np.float64, "f32": np.float32}
 
 
@@ -94,6 +98,11 @@ def load():
     L.rt_scene_stats.argtypes = [P, ctypes.POINTER(RtStats)]
     L.rt_render_async.argtypes = [P, ctypes.POINTER(RtCameraSettings), ctypes.c_uint64, ctypes.POINTER(RtExec), P, P]
     L.rt_encode8_async.argtypes = [P, ctypes.c_int32, P, ctypes.c_int64, ctypes.c_int32, P]
+    L.rt_multi_scene_create.argtypes = [ctypes.POINTER(RtScene), ctypes.POINTER(ctypes.c_int32), ctypes.c_int32,
+                                        ctypes.POINTER(ctypes.c_void_p)]
+    L.rt_multi_scene_destroy.argtypes = [P]
+    L.rt_multi_render.argtypes = [P, ctypes.POINTER(RtCameraSettings), ctypes.c_uint64, ctypes.POINTER(RtExec), P,
+                                  ctypes.POINTER(RtStats)]
     for name in EXPORTED:
         getattr(L, name)
     if L.rt_abi_version() != ABI_VERSION:
@@ -173,12 +182,15 @@ def dtype_of(precision: str):
     return PRECISIONS[precision]
 
 
-def exec_struct(device=0, n_shards=1, shard=0, row_block=4, precision="f64", devices=None):
-    """rt_exec: the row shard, the precision and (rt_render only) a device list."""
+def exec_struct(device=0, n_shards=1, shard=0, row_block=4, precision="f64", devices=None, encode=None):
+    """rt_exec: the row shard, the precision, (rt_render only) a device list and an 8-bit output
+    encoding (None: linear RGB; "srgb": writeImage's codes; "sqrt": writeImageSqrt's)."""
     dtype_of(precision)
+    if encode not in ENCODINGS:
+        raise ValueError(f"encode must be one of {sorted(k for k in ENCODINGS if k)} or None, not {encode!r}")
     e = RtExec()
     e.device, e.n_shards, e.shard, e.row_block = device, n_shards, shard, row_block
-    e.flags = RT_EXEC_F32 if precision == "f32" else 0
+    e.flags = (RT_EXEC_F32 if precision == "f32" else 0) | ENCODINGS[encode]
     if devices:
         arr = (ctypes.c_int32 * len(devices))(*[int(d) for d in devices])
         e.n_devices, e.devices = len(devices), ctypes.cast(arr, ctypes.POINTER(ctypes.c_int32))

@@ -1,6 +1,9 @@
-// rt_api.hip — the C-ABI entry points of include/rt.h: scene build (rt_build.cpp), upload to
-// HBM (both precisions' records), kernel launch (rt_kernel.hip / rt_kernel64.hip), the device
-// list of rt_render (one process, many GPUs), error reporting.
+// rt_api.hip — the C-ABI entry points of include/rt.h: scene build (rt_build.cpp, once per
+// call however many devices render), upload to HBM (a precision's records on its first render),
+// kernel launch (rt_kernel.hip / rt_kernel64.hip), multi-device scenes (one process, many GPUs:
+// concurrent uploads, shard renders on per-device streams, a device-side gather by peer copies
+// into the first device's framebuffer and ONE device-to-host copy), the 8-bit output epilogue,
+// error reporting.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -9,8 +12,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt.h"
@@ -89,8 +94,13 @@ struct rt_device_scene {
   float* nodes = nullptr;
   int* perlin_perm = nullptr;
   int* status = nullptr;
-  DevArrays<float> f32;
-  DevArrays<double> f64;
+  // a precision's records are uploaded (and its kernel's occupancy queried) on its first render:
+  // a caller that renders one precision never pays for the other's copy in HBM or its upload
+  std::shared_ptr<const HostScene> host;
+  mutable std::mutex mu;
+  mutable DevArrays<float> f32;
+  mutable DevArrays<double> f64;
+  mutable bool have_f32 = false, have_f64 = false;
   int leaf_exit_pct = 100;
   int trav_exit_pct = 50;
   int surface_root = RT_EMPTY_ROOT;
@@ -100,21 +110,63 @@ struct rt_device_scene {
   int stack_depth = 1;       // LDS stack entries per lane
   int lds_nodes = 0;         // top surface-BVH nodes staged in LDS per workgroup
   int variant = RT_VAR_FLAT;  // render-kernel variant (rt_internal.h RT_VAR_*)
-  double upload_ms = 0;
+  double build_ms = 0;       // host scene build (shared by every device of a multi-device scene)
+  mutable double upload_ms = 0;  // host -> device copies of this device (common + precisions so far)
   template <class R>
-  const DevArrays<R>& arrays() const;
+  DevArrays<R>& arrays() const;
+  template <class R>
+  bool& have() const;
 };
 template <>
-const DevArrays<float>& rt_device_scene::arrays<float>() const { return f32; }
+DevArrays<float>& rt_device_scene::arrays<float>() const { return f32; }
 template <>
-const DevArrays<double>& rt_device_scene::arrays<double>() const { return f64; }
+DevArrays<double>& rt_device_scene::arrays<double>() const { return f64; }
+template <>
+bool& rt_device_scene::have<float>() const { return have_f32; }
+template <>
+bool& rt_device_scene::have<double>() const { return have_f64; }
+
+struct rt_multi_scene {
+  std::vector<int> devices;                // shard k renders on devices[k]
+  std::vector<rt_device_scene*> scenes;    // one per DISTINCT device, in first-use order
+  std::vector<int> scene_of;               // devices[k] -> scenes index
+  double build_ms = 0, upload_ms = 0;      // one host build; the uploads' wall time (concurrent)
+};
 
 namespace {
 
 // one render of the scene's records of precision R, enqueued on `stream`
+// the records of precision R on the scene's device (uploaded on first use) and their kernel's
+// resident workgroups; thread-safe
+template <class R>
+int ensure_precision(const rt_device_scene* s) {
+  std::lock_guard<std::mutex> lock(s->mu);
+  if (s->have<R>()) return RT_OK;
+  auto t0 = std::chrono::steady_clock::now();
+  HIP_TRY(hipSetDevice(s->device));
+  DevArrays<R>& A = s->arrays<R>();
+  int rc = A.upload(s->host->arrays<R>());
+  if (rc) {
+    A.release();
+    A = DevArrays<R>();
+    return rc;
+  }
+  A.resident_blocks = rt_render_resident_blocks((const KernelParamsT<R>*)nullptr, s->device, s->stack_depth,
+                                                s->variant, s->lds_nodes);
+  if (A.resident_blocks <= 0) {
+    A.release();
+    A = DevArrays<R>();
+    return fail(RT_E_HIP, "occupancy query failed");
+  }
+  s->have<R>() = true;
+  s->upload_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return RT_OK;
+}
+
 template <class R>
 int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex, R* d_out,
                  void* hip_stream) {
+  if (int rc = ensure_precision<R>(s)) return rc;
   const DevArrays<R>& A = s->arrays<R>();
   KernelParamsT<R> P;
   std::memset(&P, 0, sizeof P);
@@ -170,6 +222,309 @@ int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_
 
 bool exec_f32(const rt_exec* ex) { return ex && (ex->flags & RT_EXEC_F32) != 0; }
 
+// rt_exec.flags -> the 8-bit epilogue's encoding (0 sRGB, 1 sqrt) or -1 (linear output)
+int exec_encoding(const rt_exec* ex) {
+  if (!ex) return -1;
+  if (ex->flags & RT_EXEC_ENCODE8_SRGB) return 0;
+  if (ex->flags & RT_EXEC_ENCODE8_SQRT) return 1;
+  return -1;
+}
+
+const double* encode8_table(int encoding) {
+  static double thr[2][256];
+  static std::once_flag once[2];
+  std::call_once(once[encoding], [&] { rt_host_encode8_thresholds(encoding, thr[encoding]); });
+  return thr[encoding];
+}
+
+void destroy_scene(rt_device_scene* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->device);
+  (void)hipFree(s->nodes);
+  (void)hipFree(s->perlin_perm);
+  (void)hipFree(s->status);
+  s->f32.release();
+  s->f64.release();
+  delete s;
+}
+
+// the precision-independent part of a device scene: BVH nodes, Perlin permutations, status word,
+// the kernel variant and the LDS plan; precisions follow on first render (ensure_precision)
+int upload_common(const std::shared_ptr<const HostScene>& Hp, int device, rt_device_scene** out) {
+  auto t0 = std::chrono::steady_clock::now();
+  const HostScene& H = *Hp;
+  *out = nullptr;
+  HIP_TRY(hipSetDevice(device));
+  auto* s = new rt_device_scene();
+  s->device = device;
+  s->host = Hp;
+  std::vector<int> status(4, 0);
+  int rc;
+  if ((rc = upload(&s->nodes, H.nodes)) || (rc = upload(&s->perlin_perm, H.perlin_perm)) ||
+      (rc = upload(&s->status, status))) {
+    destroy_scene(s);
+    return rc;
+  }
+  s->surface_root = H.surface_root;
+  s->leaf_exit_pct = H.leaf_exit_pct;
+  s->trav_exit_pct = H.trav_exit_pct;
+  s->n_media = H.n_media;
+  for (int k = 0; k <= RT_MAX_MEDIA; ++k) s->flat_sets[k] = H.flat_sets[k];
+  s->n_nodes = H.n_nodes;
+  s->n_prims = H.n_prims;
+  s->max_depth = H.max_depth;
+  s->stack_depth = H.max_depth > 1 ? H.max_depth : 1;
+  s->variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex, H.n_instances > 0);
+  if ((s->variant & RT_VAR_BASE) != RT_VAR_FLAT) {
+    // stage as many top (breadth-first) surface nodes as fit beside the stacks in the per-
+    // workgroup budget; env RT_AMD_LDS_NODES caps it (0 disables, for experiments)
+    const int room = (RT_LDS_WG_BUDGET - (s->stack_depth + 1) * RT_BLOCK_BVH * (int)sizeof(int)) / 64;
+    s->lds_nodes = std::max(0, std::min(H.surface_nodes, room));
+    if (const char* e = std::getenv("RT_AMD_LDS_NODES")) s->lds_nodes = std::min(s->lds_nodes, std::max(0, atoi(e)));
+  }
+  s->upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *out = s;
+  return RT_OK;
+}
+
+int ensure_precisions(const rt_device_scene* s, int prec_mask) {  // bit 0: FP32, bit 1: binary64
+  int rc = RT_OK;
+  if ((prec_mask & 1) && (rc = ensure_precision<float>(s))) return rc;
+  if ((prec_mask & 2) && (rc = ensure_precision<double>(s))) return rc;
+  return RT_OK;
+}
+
+int check_device(int device) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RT_E_HIP, "no HIP device");
+  if (device < 0 || device >= ndev) return fail(RT_E_INVALID, "device %d out of range (%d devices)", device, ndev);
+  return RT_OK;
+}
+
+// A multi-device scene from one host build: the distinct devices upload CONCURRENTLY (one host
+// thread each; the host build is shared, never repeated per device).  prec_mask: precisions to
+// upload now (the rest on first render).
+int multi_create(const std::shared_ptr<const HostScene>& H, const int32_t* devices, int n, int prec_mask,
+                 rt_multi_scene** out) {
+  *out = nullptr;
+  if (n < 1 || n > RT_MAX_DEVICES || !devices) return fail(RT_E_INVALID, "invalid device list (%d devices)", n);
+  for (int k = 0; k < n; ++k)
+    if (int rc = check_device(devices[k])) return rc;
+  auto* M = new rt_multi_scene();
+  M->devices.assign(devices, devices + n);
+  std::vector<int> distinct;
+  for (int k = 0; k < n; ++k) {
+    int j = (int)(std::find(distinct.begin(), distinct.end(), devices[k]) - distinct.begin());
+    if (j == (int)distinct.size()) distinct.push_back(devices[k]);
+    M->scene_of.push_back(j);
+  }
+  M->scenes.assign(distinct.size(), nullptr);
+  std::vector<int> rcs(distinct.size(), RT_OK);
+  std::vector<std::string> errs(distinct.size());
+  auto t0 = std::chrono::steady_clock::now();
+  {
+    std::vector<std::thread> th;
+    for (size_t j = 0; j < distinct.size(); ++j)
+      th.emplace_back([&, j] {
+        int rc = upload_common(H, distinct[j], &M->scenes[j]);
+        if (!rc) rc = ensure_precisions(M->scenes[j], prec_mask);
+        rcs[j] = rc;
+        if (rc) errs[j] = g_err;
+      });
+    for (auto& t : th) t.join();
+  }
+  M->upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  for (size_t j = 0; j < distinct.size(); ++j)
+    if (rcs[j]) {
+      for (rt_device_scene* s : M->scenes) destroy_scene(s);
+      delete M;
+      return fail(rcs[j], "device %d: %s", distinct[j], errs[j].c_str());
+    }
+  // the first device gathers the shard tiles: let every other device write into its memory
+  // over xGMI (peer access; without it HIP stages the copies itself)
+  for (size_t j = 1; j < distinct.size(); ++j) {
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, distinct[j], distinct[0]) == hipSuccess && can) {
+      (void)hipSetDevice(distinct[j]);
+      (void)hipDeviceEnablePeerAccess(distinct[0], 0);  // hipErrorPeerAccessAlreadyEnabled is fine
+      (void)hipGetLastError();
+    }
+  }
+  *out = M;
+  return RT_OK;
+}
+
+void multi_destroy(rt_multi_scene* M) {
+  if (!M) return;
+  for (rt_device_scene* s : M->scenes) destroy_scene(s);
+  delete M;
+}
+
+// Render the image (device list: shard k of n on devices[k]) or, with one device, the rt_exec
+// shard; gather on the first device; optional 8-bit epilogue there; ONE copy to the host buffer.
+int multi_render(const rt_multi_scene* M, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex,
+                 void* out_host, rt_stats* stats, double build_ms) {
+  auto t0 = std::chrono::steady_clock::now();
+  const int h = rt_host_image_height(cs);
+  if (h <= 0 || cs->image_width <= 0) return fail(RT_E_INVALID, "image %dx%d must be non-empty", cs->image_width, h);
+  const int n = (int)M->devices.size();
+  if (n > 1 && ex->n_shards != 1) return fail(RT_E_INVALID, "a device list renders the whole image (n_shards must be 1)");
+  const int rows_out = rt_host_shard_rows(h, ex);  // == h for a device list / a single shard
+  if (rows_out < 0) return fail(RT_E_INVALID, "invalid rt_exec");
+  {  // validate the camera before touching a device
+    KernelParams P;
+    std::string err;
+    int rc = rt_host_make_params(cs, seed, ex, P, err);
+    if (rc) return fail(rc, "%s", err.c_str());
+  }
+  const bool f32 = exec_f32(ex);
+  const int encoding = exec_encoding(ex);
+  const size_t esize = f32 ? sizeof(float) : sizeof(double);
+  const size_t row_bytes = (size_t)cs->image_width * 3 * esize;
+  struct Part {
+    rt_exec ex{};
+    int rows = 0;
+    void* d_tile = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    float ms = 0;
+    int rc = RT_OK;
+    std::string err;
+    double prep_ms = 0;
+  };
+  std::vector<Part> parts(n);
+  for (int k = 0; k < n; ++k) {
+    Part& p = parts[k];
+    p.ex = *ex;
+    p.ex.n_devices = 0;
+    p.ex.devices = nullptr;
+    p.ex.device = M->devices[k];
+    if (n > 1) {
+      p.ex.n_shards = n;
+      p.ex.shard = k;
+    }
+    p.rows = rt_host_shard_rows(h, &p.ex);
+  }
+  // the first device's framebuffer: n shard tiles in global row order (n > 1; padded to equal
+  // tiles), or the single shard's tile itself
+  const int dev0 = M->devices[0];
+  const int rb = ex->row_block;
+  const size_t gather_rows = n > 1 ? (size_t)n * parts[0].rows : (size_t)rows_out;
+  void* d_gather = nullptr;
+  uint8_t* d_codes = nullptr;
+  hipStream_t st0 = nullptr;
+  int rc = RT_OK;
+  if (hipSetDevice(dev0) != hipSuccess || hipStreamCreateWithFlags(&st0, hipStreamNonBlocking) != hipSuccess)
+    rc = fail(RT_E_HIP, "stream on device %d", dev0);
+  if (!rc && n > 1 && hipMalloc(&d_gather, gather_rows * row_bytes) != hipSuccess)
+    rc = fail(RT_E_HIP, "hipMalloc(gather %zu bytes) failed", gather_rows * row_bytes);
+  if (!rc && encoding >= 0 && hipMalloc((void**)&d_codes, std::max<size_t>(16, gather_rows * cs->image_width * 3)) != hipSuccess)
+    rc = fail(RT_E_HIP, "hipMalloc(codes) failed");
+  if (!rc) {
+    std::vector<std::thread> th;
+    for (int k = 0; k < n; ++k)
+      th.emplace_back([&, k] {
+        Part& p = parts[k];
+        const rt_device_scene* s = M->scenes[M->scene_of[k]];
+        auto run = [&]() -> int {
+          HIP_TRY(hipSetDevice(s->device));
+          auto tp = std::chrono::steady_clock::now();
+          if (int r = ensure_precisions(s, f32 ? 1 : 2)) return r;
+          p.prep_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp).count();
+          const size_t bytes = (size_t)p.rows * row_bytes;
+          HIP_TRY(hipMalloc(&p.d_tile, bytes ? bytes : 16));
+          HIP_TRY(hipStreamCreateWithFlags(&p.st, hipStreamNonBlocking));
+          HIP_TRY(hipEventCreate(&p.e0));
+          HIP_TRY(hipEventCreate(&p.e1));
+          HIP_TRY(hipEventRecord(p.e0, p.st));
+          if (int r = rt_render_async(s, cs, seed, &p.ex, p.d_tile, p.st)) return r;
+          HIP_TRY(hipEventRecord(p.e1, p.st));
+          if (n > 1) {
+            // shard-local row block b is global block b n + k: one strided copy into the first
+            // device's framebuffer (peer-to-peer over xGMI for another device)
+            const size_t w = (size_t)rb * row_bytes;
+            HIP_TRY(hipMemcpy2DAsync((char*)d_gather + (size_t)k * w, (size_t)n * w, p.d_tile, w, w,
+                                     (size_t)p.rows / rb, hipMemcpyDeviceToDevice, p.st));
+          }
+          HIP_TRY(hipStreamSynchronize(p.st));
+          HIP_TRY(hipEventElapsedTime(&p.ms, p.e0, p.e1));
+          return RT_OK;
+        };
+        p.rc = run();
+        if (p.rc) p.err = g_err;
+      });
+    for (auto& t : th) t.join();
+    for (int k = 0; k < n && !rc; ++k)
+      if (parts[k].rc) rc = fail(parts[k].rc, "device %d: %s", M->devices[k], parts[k].err.c_str());
+  }
+  int status = 0;
+  for (size_t j = 0; j < M->scenes.size() && !rc; ++j) {
+    int ps = 0;
+    (void)hipSetDevice(M->scenes[j]->device);
+    if (hipMemcpy(&ps, M->scenes[j]->status, 4, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(RT_E_HIP, "status");
+    status |= ps;
+  }
+  if (!rc && status) rc = fail(RT_E_STACK, "BVH traversal stack overflow");
+  const void* d_img = n > 1 ? d_gather : parts[0].d_tile;
+  const size_t out_rows = n > 1 ? (size_t)h : (size_t)rows_out;
+  if (!rc) {
+    (void)hipSetDevice(dev0);
+    const void* src = d_img;
+    size_t bytes = out_rows * row_bytes;
+    if (encoding >= 0) {
+      const int64_t nv = (int64_t)out_rows * cs->image_width * 3;
+      if (rt_launch_encode8(d_img, f32 ? 0 : 1, d_codes, nv, encode8_table(encoding), encoding, st0))
+        rc = fail(RT_E_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
+      src = d_codes;
+      bytes = (size_t)nv;
+    }
+    if (!rc && (hipMemcpyAsync(out_host, src, bytes, hipMemcpyDeviceToHost, st0) != hipSuccess ||
+                hipStreamSynchronize(st0) != hipSuccess))
+      rc = fail(RT_E_HIP, "copy back: %s", hipGetErrorString(hipGetLastError()));
+  }
+  if (stats && !rc) {
+    std::memset(stats, 0, sizeof *stats);
+    double prep = 0;
+    float ms = 0;
+    for (const Part& p : parts) {
+      prep = std::max(prep, p.prep_ms);
+      ms = std::max(ms, p.ms);
+    }
+    stats->upload_ms = build_ms + M->upload_ms + prep;
+    stats->kernel_ms = ms;
+    stats->samples = (int64_t)rows_out * cs->image_width * cs->samples_per_pixel;
+    stats->bvh_nodes = M->scenes[0]->n_nodes;
+    stats->max_stack = M->scenes[0]->max_depth;
+    stats->total_ms = build_ms + std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  for (int k = 0; k < n; ++k) {
+    Part& p = parts[k];
+    (void)hipSetDevice(M->devices[k]);
+    if (p.st) (void)hipStreamSynchronize(p.st);
+    if (p.e0) (void)hipEventDestroy(p.e0);
+    if (p.e1) (void)hipEventDestroy(p.e1);
+    if (p.st) (void)hipStreamDestroy(p.st);
+    (void)hipFree(p.d_tile);
+  }
+  (void)hipSetDevice(dev0);
+  if (st0) (void)hipStreamDestroy(st0);
+  (void)hipFree(d_gather);
+  (void)hipFree(d_codes);
+  return rc;
+}
+
+int build_host(const rt_scene* sc, std::shared_ptr<const HostScene>& out, double& ms) {
+  auto t0 = std::chrono::steady_clock::now();
+  auto H = std::make_shared<HostScene>();
+  std::string err;
+  int rc = rt_host_build_scene(sc, *H, err);
+  if (rc) return fail(rc, "%s", err.c_str());
+  out = H;
+  ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return RT_OK;
+}
+
+
 }  // namespace
 
 extern "C" {
@@ -203,71 +558,26 @@ int rt_shard_row(int32_t t, const rt_exec* ex) {
 }
 
 int rt_scene_destroy(rt_device_scene* s) {
-  if (!s) return RT_OK;
-  (void)hipSetDevice(s->device);
-  (void)hipFree(s->nodes);
-  (void)hipFree(s->perlin_perm);
-  (void)hipFree(s->status);
-  s->f32.release();
-  s->f64.release();
-  delete s;
+  destroy_scene(s);
   return RT_OK;
 }
 
 int rt_scene_create(const rt_scene* sc, int32_t device, rt_device_scene** out) {
-  auto t0 = std::chrono::steady_clock::now();
   if (!sc || !out) return fail(RT_E_INVALID, "null argument");
   *out = nullptr;
-  HostScene H;
-  std::string err;
-  int rc = rt_host_build_scene(sc, H, err);
-  if (rc) return fail(rc, "%s", err.c_str());
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RT_E_HIP, "no HIP device");
-  if (device < 0 || device >= ndev) return fail(RT_E_INVALID, "device %d out of range (%d devices)", device, ndev);
-  HIP_TRY(hipSetDevice(device));
-  auto* s = new rt_device_scene();
-  s->device = device;
-  std::vector<int> status(4, 0);
-  if ((rc = upload(&s->nodes, H.nodes)) || (rc = upload(&s->perlin_perm, H.perlin_perm)) ||
-      (rc = upload(&s->status, status)) || (rc = s->f32.upload(H.f32)) || (rc = s->f64.upload(H.f64))) {
-    rt_scene_destroy(s);
-    return rc;
-  }
-  s->surface_root = H.surface_root;
-  s->leaf_exit_pct = H.leaf_exit_pct;
-  s->trav_exit_pct = H.trav_exit_pct;
-  s->n_media = H.n_media;
-  for (int k = 0; k <= RT_MAX_MEDIA; ++k) s->flat_sets[k] = H.flat_sets[k];
-  s->n_nodes = H.n_nodes;
-  s->n_prims = H.n_prims;
-  s->max_depth = H.max_depth;
-  s->stack_depth = H.max_depth > 1 ? H.max_depth : 1;
-  s->variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex, H.n_instances > 0);
-  if ((s->variant & RT_VAR_BASE) != RT_VAR_FLAT) {
-    // stage as many top (breadth-first) surface nodes as fit beside the stacks in the per-
-    // workgroup budget; env RT_AMD_LDS_NODES caps it (0 disables, for experiments)
-    const int room = (RT_LDS_WG_BUDGET - (s->stack_depth + 1) * RT_BLOCK_BVH * (int)sizeof(int)) / 64;
-    s->lds_nodes = std::max(0, std::min(H.surface_nodes, room));
-    if (const char* e = std::getenv("RT_AMD_LDS_NODES")) s->lds_nodes = std::min(s->lds_nodes, std::max(0, atoi(e)));
-  }
-  s->f32.resident_blocks =
-      rt_render_resident_blocks((const KernelParams*)nullptr, device, s->stack_depth, s->variant, s->lds_nodes);
-  s->f64.resident_blocks =
-      rt_render_resident_blocks((const KernelParams64*)nullptr, device, s->stack_depth, s->variant, s->lds_nodes);
-  if (s->f32.resident_blocks <= 0 || s->f64.resident_blocks <= 0) {
-    rt_scene_destroy(s);
-    return fail(RT_E_HIP, "occupancy query failed");
-  }
-  s->upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  *out = s;
+  std::shared_ptr<const HostScene> H;
+  double build_ms = 0;
+  if (int rc = build_host(sc, H, build_ms)) return rc;
+  if (int rc = check_device(device)) return rc;
+  if (int rc = upload_common(H, device, out)) return rc;
+  (*out)->build_ms = build_ms;
   return RT_OK;
 }
 
 int rt_scene_stats(const rt_device_scene* s, rt_stats* st) {
   if (!s || !st) return fail(RT_E_INVALID, "null argument");
   std::memset(st, 0, sizeof *st);
-  st->upload_ms = s->upload_ms;
+  st->upload_ms = s->build_ms + s->upload_ms;
   st->bvh_nodes = s->n_nodes;
   st->max_stack = s->stack_depth;
   return RT_OK;
@@ -275,135 +585,67 @@ int rt_scene_stats(const rt_device_scene* s, rt_stats* st) {
 
 int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex,
                     void* d_out_rgb, void* hip_stream) {
-  if (!s || !d_out_rgb || !ex) return fail(RT_E_INVALID, "null argument");
+  if (!s || !d_out_rgb || !ex || !cs) return fail(RT_E_INVALID, "null argument");
   if (ex->n_devices != 0) return fail(RT_E_INVALID, "rt_render_async renders on the scene's device (n_devices = 0)");
+  if (exec_encoding(ex) >= 0) return fail(RT_E_INVALID, "rt_render_async writes linear RGB (use rt_encode8_async)");
   if (exec_f32(ex)) return render_async<float>(s, cs, seed, ex, (float*)d_out_rgb, hip_stream);
   return render_async<double>(s, cs, seed, ex, (double*)d_out_rgb, hip_stream);
 }
 
+int rt_multi_scene_create(const rt_scene* sc, const int32_t* devices, int32_t n_devices, rt_multi_scene** out) {
+  if (!sc || !out) return fail(RT_E_INVALID, "null argument");
+  *out = nullptr;
+  std::shared_ptr<const HostScene> H;
+  double build_ms = 0;
+  if (int rc = build_host(sc, H, build_ms)) return rc;
+  if (int rc = multi_create(H, devices, n_devices, 0, out)) return rc;
+  (*out)->build_ms = build_ms;
+  return RT_OK;
+}
+
+int rt_multi_scene_destroy(rt_multi_scene* m) {
+  multi_destroy(m);
+  return RT_OK;
+}
+
+int rt_multi_render(const rt_multi_scene* m, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex,
+                    void* out, rt_stats* stats) {
+  if (!m || !cs || !ex || !out) return fail(RT_E_INVALID, "null argument");
+  if (ex->n_devices != 0) return fail(RT_E_INVALID, "rt_multi_render renders on the scene's devices (n_devices = 0)");
+  const int rc = multi_render(m, cs, seed, ex, out, stats, 0.0);
+  if (!rc && stats) stats->upload_ms += m->build_ms;  // the scene's one-time cost, as rt_render reports it
+  return rc;
+}
+
 int rt_render(const rt_camera_settings* cs, const rt_scene* scene, uint64_t seed, const rt_exec* ex, void* out_rgb,
               rt_stats* stats) {
-  auto t0 = std::chrono::steady_clock::now();
   if (!cs || !scene || !ex || !out_rgb) return fail(RT_E_INVALID, "null argument");
   int h = rt_host_image_height(cs);
   if (h <= 0 || cs->image_width <= 0) return fail(RT_E_INVALID, "image %dx%d must be non-empty", cs->image_width, h);
-  int rows = rt_host_shard_rows(h, ex);
-  if (rows < 0) return fail(RT_E_INVALID, "invalid rt_exec");
+  if (rt_host_shard_rows(h, ex) < 0) return fail(RT_E_INVALID, "invalid rt_exec");
   if (ex->n_devices < 0 || ex->n_devices > RT_MAX_DEVICES || (ex->n_devices > 0 && !ex->devices))
     return fail(RT_E_INVALID, "invalid device list (%d devices)", ex->n_devices);
   if (ex->n_devices > 0 && ex->n_shards != 1)
     return fail(RT_E_INVALID, "a device list renders the whole image (n_shards must be 1)");
-  {  // validate the camera before touching a device
+  {  // validate the camera before building or touching a device
     KernelParams P;
     std::string err;
     int rc = rt_host_make_params(cs, seed, ex, P, err);
     if (rc) return fail(rc, "%s", err.c_str());
   }
-  const bool f32 = exec_f32(ex);
-  const size_t esize = f32 ? sizeof(float) : sizeof(double);
-  const size_t row_bytes = (size_t)cs->image_width * 3 * esize;
-  // the parts of this call: one (the rt_exec shard on `device`), or shard k of n_devices on
-  // devices[k]; each part renders into its own device buffer on its own stream, concurrently
-  const int n_parts = ex->n_devices > 0 ? ex->n_devices : 1;
-  struct Part {
-    int device = 0;
-    rt_exec ex{};
-    int rows = 0;
-    rt_device_scene* scene = nullptr;  // owned by the first part on its device
-    bool owns_scene = false;
-    void* d_out = nullptr;
-    hipStream_t st = nullptr;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    std::vector<char> host;
-  };
-  std::vector<Part> parts(n_parts);
-  int rc = RT_OK;
-  for (int k = 0; k < n_parts && !rc; ++k) {
-    Part& p = parts[k];
-    p.ex = *ex;
-    p.ex.n_devices = 0;
-    p.ex.devices = nullptr;
-    if (ex->n_devices > 0) {
-      p.device = ex->devices[k];
-      p.ex.device = p.device;
-      p.ex.n_shards = n_parts;
-      p.ex.shard = k;
-    } else {
-      p.device = ex->device;
-    }
-    p.rows = rt_host_shard_rows(h, &p.ex);
-    for (int j = 0; j < k; ++j)
-      if (parts[j].device == p.device) p.scene = parts[j].scene;  // one upload per device
-    if (!p.scene) {
-      if ((rc = rt_scene_create(scene, p.device, &p.scene))) break;
-      p.owns_scene = true;
-    }
-    if (hipSetDevice(p.device) != hipSuccess) {
-      rc = fail(RT_E_HIP, "hipSetDevice(%d) failed", p.device);
-      break;
-    }
-    const size_t bytes = (size_t)p.rows * row_bytes;
-    if (hipMalloc(&p.d_out, bytes ? bytes : 16) != hipSuccess) rc = fail(RT_E_HIP, "hipMalloc(%zu) failed", bytes);
-    if (!rc && hipStreamCreateWithFlags(&p.st, hipStreamNonBlocking) != hipSuccess) rc = fail(RT_E_HIP, "stream create");
-    if (!rc && (hipEventCreate(&p.e0) != hipSuccess || hipEventCreate(&p.e1) != hipSuccess)) rc = fail(RT_E_HIP, "events");
-    if (!rc) {
-      (void)hipEventRecord(p.e0, p.st);
-      rc = rt_render_async(p.scene, cs, seed, &p.ex, p.d_out, p.st);
-      (void)hipEventRecord(p.e1, p.st);
-    }
-  }
-  float ms = 0;
-  int status = 0;
-  for (int k = 0; k < n_parts && !rc; ++k) {  // every part is in flight: wait, copy back
-    Part& p = parts[k];
-    float pm = 0;
-    int ps = 0;
-    (void)hipSetDevice(p.device);
-    if (hipStreamSynchronize(p.st) != hipSuccess)
-      rc = fail(RT_E_HIP, "render on device %d failed: %s", p.device, hipGetErrorString(hipGetLastError()));
-    if (!rc) (void)hipEventElapsedTime(&pm, p.e0, p.e1);
-    ms = std::max(ms, pm);
-    const size_t bytes = (size_t)p.rows * row_bytes;
-    void* dst = out_rgb;
-    if (n_parts > 1) {
-      p.host.resize(bytes);
-      dst = p.host.data();
-    }
-    if (!rc && hipMemcpy(dst, p.d_out, bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(RT_E_HIP, "copy back");
-    if (!rc && hipMemcpy(&ps, p.scene->status, 4, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(RT_E_HIP, "status");
-    status |= ps;
-  }
-  if (!rc && status) rc = fail(RT_E_STACK, "BVH traversal stack overflow");
-  if (!rc && n_parts > 1) {  // gather: shard-local row t of part k is global row rt_shard_row(t)
-    for (int k = 0; k < n_parts; ++k) {
-      const Part& p = parts[k];
-      for (int t = 0; t < p.rows; ++t) {
-        const int y = ((t / p.ex.row_block) * p.ex.n_shards + p.ex.shard) * p.ex.row_block + (t % p.ex.row_block);
-        if (y < h) std::memcpy((char*)out_rgb + (size_t)y * row_bytes, p.host.data() + (size_t)t * row_bytes, row_bytes);
-      }
-    }
-  }
-  if (stats && !rc) {
-    std::memset(stats, 0, sizeof *stats);
-    for (const Part& p : parts)
-      if (p.owns_scene) stats->upload_ms += p.scene->upload_ms;
-    stats->kernel_ms = ms;
-    stats->samples = (int64_t)rows * cs->image_width * cs->samples_per_pixel;
-    stats->bvh_nodes = parts[0].scene->n_nodes;
-    stats->max_stack = parts[0].scene->max_depth;
-    stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  }
-  for (Part& p : parts) {
-    if (!p.scene) continue;
-    (void)hipSetDevice(p.device);
-    if (p.st) (void)hipStreamSynchronize(p.st);
-    if (p.e0) (void)hipEventDestroy(p.e0);
-    if (p.e1) (void)hipEventDestroy(p.e1);
-    if (p.st) (void)hipStreamDestroy(p.st);
-    (void)hipFree(p.d_out);
-  }
-  for (Part& p : parts)
-    if (p.owns_scene) rt_scene_destroy(p.scene);
+  std::shared_ptr<const HostScene> H;
+  double build_ms = 0;
+  if (int rc = build_host(scene, H, build_ms)) return rc;  // ONE host build, whatever the device count
+  const int32_t one = ex->device;
+  const int32_t* devs = ex->n_devices > 0 ? ex->devices : &one;
+  const int n = ex->n_devices > 0 ? ex->n_devices : 1;
+  rt_multi_scene* M = nullptr;
+  if (int rc = multi_create(H, devs, n, exec_f32(ex) ? 1 : 2, &M)) return rc;  // only this call's precision
+  rt_exec e = *ex;
+  e.n_devices = 0;
+  e.devices = nullptr;
+  const int rc = multi_render(M, cs, seed, &e, out_rgb, stats, build_ms);
+  multi_destroy(M);
   return rc;
 }
 
@@ -411,10 +653,7 @@ int rt_encode8_async(const void* d_rgb, int32_t in_f64, uint8_t* d_out, int64_t 
                      void* hip_stream) {
   if (!d_rgb || !d_out || n_values < 0) return fail(RT_E_INVALID, "invalid encode arguments");
   if (encoding != 0 && encoding != 1) return fail(RT_E_INVALID, "encoding must be 0 (sRGB) or 1 (sqrt)");
-  static double thr[2][256];
-  static std::once_flag once[2];
-  std::call_once(once[encoding], [&] { rt_host_encode8_thresholds(encoding, thr[encoding]); });
-  if (rt_launch_encode8(d_rgb, in_f64 ? 1 : 0, d_out, n_values, thr[encoding], encoding, hip_stream))
+  if (rt_launch_encode8(d_rgb, in_f64 ? 1 : 0, d_out, n_values, encode8_table(encoding), encoding, hip_stream))
     return fail(RT_E_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
   return RT_OK;
 }

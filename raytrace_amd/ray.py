@@ -31,17 +31,19 @@ def _seed64(seed) -> int:
 
 
 def raytrace(settings: CameraSettings, world, seed, device: int = 0, stats: dict | None = None,
-             precision: str = "f64", devices=None, row_block: int = 4) -> np.ndarray:
+             precision: str = "f64", devices=None, row_block: int = 4, encode: str | None = None) -> np.ndarray:
     """Render on the GPU.  Returns (height, width, 3) linear RGB: float64 computed in binary64 as the
     reference does (default), or float32 from the FP32 kernel (precision="f32").  `devices`: a list
     of HIP devices that render the image together from this process (rt_exec device list; rows
-    dealt round-robin in blocks of `row_block`); the image is identical to the one-device render."""
+    dealt round-robin in blocks of `row_block`); the image is identical to the one-device render.
+    `encode` = "srgb" / "sqrt": uint8 codes as writeImage / writeImageSqrt store them, encoded on
+    the device after the gather (Ray.hs:248-260; equal to encode8 of the linear render)."""
     L = _lib.load()
     flat = world if isinstance(world, FlatScene) else flatten(world)
     cs = _lib.camera_struct(settings)
     sc = _lib.scene_struct(flat)
     ex = _lib.exec_struct(device=device, precision=precision, devices=devices,
-                          row_block=row_block if devices else 4)
+                          row_block=row_block if devices else 4, encode=encode)
     h = image_height(settings)
     w = int(settings.cs_imageWidth)
     if h <= 0 or w <= 0:
@@ -50,7 +52,7 @@ def raytrace(settings: CameraSettings, world, seed, device: int = 0, stats: dict
     rows = _lib.check(L.rt_shard_rows(h, ctypes.byref(ex)))
     if rows != h:
         raise RuntimeError(f"librt_amd.so reports {rows} rows for a {h}-row image")
-    out = np.zeros((h, w, 3), _lib.dtype_of(precision))
+    out = np.zeros((h, w, 3), np.uint8 if encode else _lib.dtype_of(precision))
     st = _lib.RtStats()
     _lib.check(L.rt_render(ctypes.byref(cs), ctypes.byref(sc), _seed64(seed), ctypes.byref(ex),
                            out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st)))
@@ -132,6 +134,46 @@ class DeviceScene:
     def close(self):
         if self.handle:
             self._lib.rt_scene_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MultiDeviceScene:
+    """A scene resident on a list of GPUs of this process (rt_multi_scene_create: one host build,
+    concurrent uploads).  `render` returns the whole image like `raytrace(..., devices=...)`,
+    without rebuilding or re-uploading the scene; shard k renders on devices[k]."""
+
+    def __init__(self, world, devices):
+        self._lib = _lib.load()
+        self.flat = world if isinstance(world, FlatScene) else flatten(world)
+        self.devices = [int(d) for d in devices]
+        sc = _lib.scene_struct(self.flat)
+        arr = (ctypes.c_int32 * len(self.devices))(*self.devices)
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.rt_multi_scene_create(ctypes.byref(sc), arr, len(self.devices), ctypes.byref(h)))
+        self.handle = h
+
+    def render(self, settings: CameraSettings, seed, precision: str = "f64", row_block: int = 4,
+               encode: str | None = None, stats: dict | None = None) -> np.ndarray:
+        cs = _lib.camera_struct(settings)
+        ex = _lib.exec_struct(device=self.devices[0], precision=precision, row_block=row_block, encode=encode)
+        h, w = image_height(settings), int(settings.cs_imageWidth)
+        out = np.zeros((h, w, 3), np.uint8 if encode else _lib.dtype_of(precision))
+        st = _lib.RtStats()
+        _lib.check(self._lib.rt_multi_render(self.handle, ctypes.byref(cs), _seed64(seed), ctypes.byref(ex),
+                                             out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st)))
+        if stats is not None:
+            stats.update(upload_ms=st.upload_ms, kernel_ms=st.kernel_ms, total_ms=st.total_ms, samples=st.samples)
+        return out
+
+    def close(self):
+        if self.handle:
+            self._lib.rt_multi_scene_destroy(self.handle)
             self.handle = None
 
     def __del__(self):

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
     exported = set(re.findall(r"\bT (rt_\w+)", out.stdout))
     assert set(names) <= exported
-    assert L.rt_abi_version() == _lib.ABI_VERSION == 3
+    assert L.rt_abi_version() == _lib.ABI_VERSION == 4
 
 
 def test_host_only_entry_points_without_gpu():
@@ -172,3 +172,23 @@ def test_haskell_binding_offsets_match_header():
     imports = re.findall(r'foreign import ccall (?:safe|unsafe) "(\w+)"', hs)
     assert set(imports) <= set(_lib.EXPORTED) and "rt_render" in imports
     assert 'error "' not in hs  # no unimplemented stubs
+
+
+def test_haskell_binding_needs_no_reference_edit():
+    """Device.hs embeds Noise.hs's permutation constants (the reference does not export them) and
+    re-exports the reference's raw constructors as bundled pattern synonyms (custom geometries,
+    materials and textures compile unchanged and render through the CPU fallback)."""
+    import json
+    hs = open(os.path.join(ROOT, "hs", "Graphics", "Ray", "Device.hs")).read()
+    assert "import Graphics.Ray.Noise" not in hs
+    with open(os.path.join(ROOT, "raytrace_amd", "data", "perlin_perm.json")) as f:
+        perm = json.load(f)
+    for name in ("permX", "permY", "permZ"):
+        m = re.search(name + r"Table =\s*\[([^\]]*)\]", hs)
+        assert m, name
+        assert [int(x) for x in m.group(1).replace("\n", " ").split(",")] == perm[name], name
+    for con in ("Geometry", "Material", "Texture"):
+        assert f"{con}({con})" in hs and f"pattern {con} ::" in hs, con
+        assert f"fromReference{con}" in hs
+    # RT_E_UNSUPPORTED (-3) and RT_E_STACK (-5) go to the CPU path
+    assert "code == -3 || code == -5" in hs

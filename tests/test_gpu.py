@@ -308,6 +308,32 @@ def test_deterministic_shard_and_device_list_invariant(gpu, precision):
     assert not np.array_equal(a, d)
 
 
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_multi_device_scene_and_encoded_output(gpu, precision):
+    """rt_multi_scene: one host build, resident across renders (no rebuild or re-upload on the
+    second render), gather into the first device's framebuffer, and the 8-bit epilogue fused
+    after the gather (rt_exec RT_EXEC_ENCODE8_*): bytes equal encode8 of the linear render."""
+    cs, world, seed = scenes.bunny_cornell(width=64, spp=4)
+    a = R.raytrace(cs, world, seed, precision=precision)
+    for enc in ("srgb", "sqrt"):
+        np.testing.assert_array_equal(R.raytrace(cs, world, seed, precision=precision, encode=enc), R.encode8(a, enc))
+        np.testing.assert_array_equal(R.raytrace(cs, world, seed, precision=precision, encode=enc, devices=[0, 0, 0],
+                                                 row_block=2), R.encode8(a, enc))
+    m = R.MultiDeviceScene(world, [0] * 8)
+    st1, st2 = {}, {}
+    np.testing.assert_array_equal(m.render(cs, seed, precision=precision, row_block=1, stats=st1), a)
+    np.testing.assert_array_equal(m.render(cs, seed, precision=precision, row_block=3, stats=st2), a)
+    np.testing.assert_array_equal(m.render(cs, seed, precision=precision, encode="srgb"), R.encode8(a, "srgb"))
+    # the second render re-uses the resident records: only the one-time build is reported again
+    assert st2["upload_ms"] <= st1["upload_ms"] + 1.0, (st1, st2)
+    assert st1["samples"] == st2["samples"] == 64 * 64 * 4
+    m.close()
+    # one entry, rendering an rt_exec shard: the multi-device call with a single device
+    single = R.MultiDeviceScene(world, [0])
+    np.testing.assert_array_equal(single.render(cs, seed, precision=precision), a)
+    single.close()
+
+
 def test_device_list_bvh_scene(gpu):
     cs, world, seed = scenes.bunny_cornell(width=64, spp=4)
     a = R.raytrace(cs, world, seed)
