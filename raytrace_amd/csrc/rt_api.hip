@@ -399,6 +399,7 @@ int multi_render(const rt_multi_scene* M, const rt_camera_settings* cs, uint64_t
     p.ex.n_devices = 0;
     p.ex.devices = nullptr;
     p.ex.device = M->devices[k];
+    p.ex.flags &= ~(RT_EXEC_ENCODE8_SRGB | RT_EXEC_ENCODE8_SQRT);  // the tiles are linear; encoded after the gather
     if (n > 1) {
       p.ex.n_shards = n;
       p.ex.shard = k;
