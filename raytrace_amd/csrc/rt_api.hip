@@ -214,7 +214,12 @@ int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_
   P.nanflag = (unsigned int*)(ws + off_flag);
   P.counter = (int*)(ws + off_ctr);
   rc = RT_OK;
-  if (rt_launch_render(P, A.resident_blocks, s->variant, hip_stream) || rt_launch_resolve(P, hip_stream))
+  // The persistent grid leaves RT_GRID_RESERVE workgroup slots free (one per XCD): when a caller
+  // overlaps frames on two streams, the next frame's grid then cannot take every slot, and this
+  // frame's resolve runs as soon as its render ends instead of queueing behind the next render.
+  int reserve = A.resident_blocks > 16 * RT_GRID_RESERVE ? RT_GRID_RESERVE : 0;
+  if (const char* e = std::getenv("RT_AMD_GRID_RESERVE")) reserve = std::max(0, std::min(A.resident_blocks - 1, atoi(e)));
+  if (rt_launch_render(P, A.resident_blocks - reserve, s->variant, hip_stream) || rt_launch_resolve(P, hip_stream))
     rc = fail(RT_E_HIP, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
   HIP_TRY(hipFreeAsync(ws, st));
   return rc;
@@ -278,7 +283,7 @@ int upload_common(const std::shared_ptr<const HostScene>& Hp, int device, rt_dev
   if ((s->variant & RT_VAR_BASE) != RT_VAR_FLAT) {
     // stage as many top (breadth-first) surface nodes as fit beside the stacks in the per-
     // workgroup budget; env RT_AMD_LDS_NODES caps it (0 disables, for experiments)
-    const int room = (RT_LDS_WG_BUDGET - (s->stack_depth + 1) * RT_BLOCK_BVH * (int)sizeof(int)) / 64;
+    const int room = (RT_LDS_WG_BUDGET - (s->stack_depth + RT_STACK_SPARE) * RT_BLOCK_BVH * (int)sizeof(int)) / 64;
     s->lds_nodes = std::max(0, std::min(H.surface_nodes, room));
     if (const char* e = std::getenv("RT_AMD_LDS_NODES")) s->lds_nodes = std::min(s->lds_nodes, std::max(0, atoi(e)));
   }
