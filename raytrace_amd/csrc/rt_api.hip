@@ -283,7 +283,7 @@ int upload_common(const std::shared_ptr<const HostScene>& Hp, int device, rt_dev
   if ((s->variant & RT_VAR_BASE) != RT_VAR_FLAT) {
     // stage as many top (breadth-first) surface nodes as fit beside the stacks in the per-
     // workgroup budget; env RT_AMD_LDS_NODES caps it (0 disables, for experiments)
-    const int room = (RT_LDS_WG_BUDGET - (s->stack_depth + RT_STACK_SPARE) * RT_BLOCK_BVH * (int)sizeof(int)) / 64;
+    const int room = (RT_LDS_WG_BUDGET - (s->stack_depth + 1) * RT_BLOCK_BVH * (int)sizeof(int)) / 64;
     s->lds_nodes = std::max(0, std::min(H.surface_nodes, room));
     if (const char* e = std::getenv("RT_AMD_LDS_NODES")) s->lds_nodes = std::min(s->lds_nodes, std::max(0, atoi(e)));
   }

@@ -1,10 +1,8 @@
-// rt_bvh.cpp — binned SAH BVH builder (host): BVH2 by binned SAH, collapsed to 4-wide nodes with
-// 8-bit quantised child boxes.  See rt_bvh.h.
+// rt_bvh.cpp — binned SAH BVH2 builder (host).  See rt_bvh.h.
 #include "rt_bvh.h"
 
 #include <algorithm>
 #include <cmath>
-#include <cstdint>
 #include <cstring>
 
 #include "rt_internal.h"
@@ -162,48 +160,6 @@ struct Builder {
 inline float f_down(double x, double pad) { return std::nextafter((float)(x - pad), -INFINITY); }
 inline float f_up(double x, double pad) { return std::nextafter((float)(x + pad), INFINITY); }
 
-// A child box as the device decodes it: plane = fma(q, s, origin) in FP32 with q an 8-bit code,
-// s = 2^e and origin = k s for an integer k with |k| + 255 < 2^24, so every decoded plane is an
-// exactly representable float (the fma is exact).  Codes round OUTWARD from the padded float box,
-// so the decoded box contains it: traversal tests a superset of the leaves the float box would
-// give, and the closest hit, keyed by (t, depth-first order), cannot change.
-struct Quant {
-  float origin[3], scale[3];
-  uint8_t lo[4][3], hi[4][3];
-};
-
-inline float decode(int q, float s, float o) { return std::fma((float)q, s, o); }
-
-// the smallest scale 2^e for which [lo, hi] fits 255 steps from an origin k 2^e with exact decode
-void axis_frame(float lo, float hi, float& origin, float& scale) {
-  int e = -140;
-  const double ext = (double)hi - (double)lo;
-  if (ext > 0) e = std::max(e, (int)std::floor(std::log2(ext / 255.0)) - 1);
-  for (;; ++e) {
-    const double s = std::ldexp(1.0, e);
-    const double k = std::floor((double)lo / s);
-    if (std::fabs(k) + 256.0 >= 16777216.0) continue;  // decode would round
-    if (std::ceil(((double)hi - k * s) / s) > 255.0) continue;
-    if (e < -126) continue;  // keep s and the planes normal floats
-    origin = (float)(k * s);
-    scale = (float)s;
-    return;
-  }
-}
-
-int code_down(float v, float s, float o) {  // largest q with decode(q) <= v
-  int q = (int)std::floor(((double)v - (double)o) / (double)s);
-  q = std::max(0, std::min(255, q));
-  while (q > 0 && decode(q, s, o) > v) --q;
-  return q;
-}
-int code_up(float v, float s, float o) {  // smallest q with decode(q) >= v
-  int q = (int)std::ceil(((double)v - (double)o) / (double)s);
-  q = std::max(0, std::min(255, q));
-  while (q < 255 && decode(q, s, o) < v) ++q;
-  return q;
-}
-
 }  // namespace
 
 void rt_build_bvh(std::vector<BuildPrim> prims, int node_base, int prim_base, BvhOut& out, int leaf_max) {
@@ -218,45 +174,25 @@ void rt_build_bvh(std::vector<BuildPrim> prims, int node_base, int prim_base, Bv
   Builder B(prims);
   B.leaf_max = leaf_max;
   int root = B.build(0, (int)prims.size(), 0);
+  out.max_depth = B.max_depth;
   // primitive slots skip the instance items (each is its own leaf, encoded as RT_INST_CODE)
   std::vector<int> slot(prims.size() + 1, 0);
   for (size_t i = 0; i < prims.size(); ++i) {
     slot[i + 1] = slot[i] + (prims[i].inst < 0 ? 1 : 0);
     if (prims[i].inst < 0) out.order.push_back(prims[i].index);
   }
-  // BVH2 -> BVH4: a node's children are its two children, then repeatedly the internal child of
-  // largest surface area is replaced by its two children, up to four (Wald et al. 2008's collapse)
-  const int T = (int)B.tmp.size();
-  std::vector<std::vector<int>> kids(T);
-  auto collapse = [&](int id) {
-    std::vector<int> c = {B.tmp[id].left, B.tmp[id].right};
-    while (c.size() < 4) {
-      int best = -1;
-      double best_area = -1.0;
-      for (int j = 0; j < (int)c.size(); ++j)
-        if (B.tmp[c[j]].left >= 0 && B.tmp[c[j]].box.area() > best_area) {
-          best_area = B.tmp[c[j]].box.area();
-          best = j;
-        }
-      if (best < 0) break;
-      const int n = c[best];
-      c[best] = B.tmp[n].left;
-      c.insert(c.begin() + best + 1, B.tmp[n].right);
-    }
-    kids[id] = c;
-  };
-  // number the 4-wide internal nodes breadth-first: the top levels are the first nodes of the
-  // set, which is what the kernel stages in LDS (KernelParams::lds_nodes)
-  std::vector<int> dev_index(T, -1);
+  // number internal nodes breadth-first: the top levels are the first nodes of the set, which
+  // is what the kernel stages in LDS (KernelParams::lds_nodes)
+  std::vector<int> dev_index(B.tmp.size(), -1);
   std::vector<int> internal;
   std::vector<int> queue = {root};
   for (size_t head = 0; head < queue.size(); ++head) {
     int id = queue[head];
     if (B.tmp[id].left < 0) continue;
-    collapse(id);
     dev_index[id] = node_base + (int)internal.size();
     internal.push_back(id);
-    for (int c : kids[id]) queue.push_back(c);
+    queue.push_back(B.tmp[id].left);
+    queue.push_back(B.tmp[id].right);
   }
   auto enc = [&](int id) -> int {
     const Node& nd = B.tmp[id];
@@ -265,72 +201,23 @@ void rt_build_bvh(std::vector<BuildPrim> prims, int node_base, int prim_base, Bv
     // leaf: ~(first << RT_LEAF_SHIFT | count - 1); leaves hold <= RT_FLAT_MAX primitives
     return ~(((prim_base + slot[nd.first]) << RT_LEAF_SHIFT) | (nd.count - 1));
   };
-  // traversal stack a root-to-leaf walk can need: a node pushes at most (children - 1) entries
-  std::vector<int> need(T, 0);
-  for (int k = (int)internal.size() - 1; k >= 0; --k) {  // children come later in breadth-first order
-    const int id = internal[k];
-    int deepest = 0;
-    for (int c : kids[id]) deepest = std::max(deepest, need[c]);
-    need[id] = (int)kids[id].size() - 1 + deepest;
-  }
-  out.max_depth = std::max(1, need[root]);
   out.n_nodes = (int)internal.size();
   out.nodes.assign((size_t)out.n_nodes * 16, 0.0f);
-  auto pad = [](const Box& b, int a) { return 1e-6 * std::max(std::fabs(b.lo[a]), std::fabs(b.hi[a])) + 1e-7; };
   for (size_t k = 0; k < internal.size(); ++k) {
-    const std::vector<int>& c = kids[internal[k]];
-    // the children's float boxes, rounded outward and padded (conservative for binary64 leaves)
-    float flo[4][3], fhi[4][3];
-    float ulo[3] = {INFINITY, INFINITY, INFINITY}, uhi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (size_t j = 0; j < c.size(); ++j) {
-      const Box& bx = B.tmp[c[j]].box;
-      for (int a = 0; a < 3; ++a) {
-        flo[j][a] = f_down(bx.lo[a], pad(bx, a));
-        fhi[j][a] = f_up(bx.hi[a], pad(bx, a));
-        ulo[a] = std::min(ulo[a], flo[j][a]);
-        uhi[a] = std::max(uhi[a], fhi[j][a]);
-      }
-    }
-    Quant Q{};
-    for (int a = 0; a < 3; ++a) axis_frame(ulo[a], uhi[a], Q.origin[a], Q.scale[a]);
-    uint32_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
-    for (size_t j = 0; j < c.size(); ++j)
-      for (int a = 0; a < 3; ++a) {
-        const int l = code_down(flo[j][a], Q.scale[a], Q.origin[a]);
-        const int h = code_up(fhi[j][a], Q.scale[a], Q.origin[a]);
-        qlo[a] |= (uint32_t)l << (8 * j);
-        qhi[a] |= (uint32_t)h << (8 * j);
-      }
-    // layout (rt_internal.h, 4 x float4): (ox, oy, oz, sx) (sy, sz, qlo.x, qhi.x)
-    // (qlo.y, qhi.y, qlo.z, qhi.z) (child 0..3); byte j of a code word is child j
+    const Node& nd = B.tmp[internal[k]];
+    const Box& L = B.tmp[nd.left].box;
+    const Box& R = B.tmp[nd.right].box;
     float* f = out.nodes.data() + 16 * k;
-    f[0] = Q.origin[0];
-    f[1] = Q.origin[1];
-    f[2] = Q.origin[2];
-    f[3] = Q.scale[0];
-    f[4] = Q.scale[1];
-    f[5] = Q.scale[2];
-    std::memcpy(&f[6], &qlo[0], 4);
-    std::memcpy(&f[7], &qhi[0], 4);
-    std::memcpy(&f[8], &qlo[1], 4);
-    std::memcpy(&f[9], &qhi[1], 4);
-    std::memcpy(&f[10], &qlo[2], 4);
-    std::memcpy(&f[11], &qhi[2], 4);
-    for (int j = 0; j < 4; ++j) {
-      const int r = j < (int)c.size() ? enc(c[j]) : RT_EMPTY_ROOT;
-      std::memcpy(&f[12 + j], &r, 4);
-    }
+    auto pad = [](const Box& b, int a) { return 1e-6 * std::max(std::fabs(b.lo[a]), std::fabs(b.hi[a])) + 1e-7; };
+    f[0] = f_down(L.lo[0], pad(L, 0)); f[1] = f_up(L.hi[0], pad(L, 0));
+    f[2] = f_down(L.lo[1], pad(L, 1)); f[3] = f_up(L.hi[1], pad(L, 1));
+    f[4] = f_down(R.lo[0], pad(R, 0)); f[5] = f_up(R.hi[0], pad(R, 0));
+    f[6] = f_down(R.lo[1], pad(R, 1)); f[7] = f_up(R.hi[1], pad(R, 1));
+    f[8] = f_down(L.lo[2], pad(L, 2)); f[9] = f_up(L.hi[2], pad(L, 2));
+    f[10] = f_down(R.lo[2], pad(R, 2)); f[11] = f_up(R.hi[2], pad(R, 2));
+    int l = enc(nd.left), r = enc(nd.right);
+    std::memcpy(&f[12], &l, 4);
+    std::memcpy(&f[13], &r, 4);
   }
   out.root = enc(root);
-}
-
-// the decoded (exact float) box of child j of a 4-wide node, as the kernel computes it
-void rt_bvh4_child_box(const float* node, int j, float lo[3], float hi[3]) {
-  uint32_t w[6];
-  std::memcpy(w, node + 6, sizeof w);
-  const float o[3] = {node[0], node[1], node[2]}, s[3] = {node[3], node[4], node[5]};
-  for (int a = 0; a < 3; ++a) {
-    lo[a] = decode((int)((w[2 * a] >> (8 * j)) & 255u), s[a], o[a]);
-    hi[a] = decode((int)((w[2 * a + 1] >> (8 * j)) & 255u), s[a], o[a]);
-  }
 }

@@ -61,9 +61,6 @@
 #ifndef RT_GRID_RESERVE
 #define RT_GRID_RESERVE 8  // render-grid workgroup slots left free for the resolve (rt_api.hip render_async)
 #endif
-// LDS stack rows above stack_depth: the branch-free 4-wide node step writes up to three pushes
-// at sp .. sp + 2 before it knows how many it keeps (rt_trace.h trav_round)
-#define RT_STACK_SPARE 3
 // Two-level instancing: a BVH child RT_INST_FLAG | k enters instance k (the ray goes to object
 // space, the object's BVH is traversed); RT_INST_EXIT, pushed on entry, returns to world space.
 // Node indices stay below RT_INST_FLAG.

@@ -179,9 +179,9 @@ void rt_render_kernel(KernelParams P) {
     overflow =
         lane_loop_lockstep<true, kTex, kMedia, kMats>(P, grab, commit, Trav{nullptr, 0, nullptr}, P.prims);
   } else {
-    // LDS: [stack_depth + RT_STACK_SPARE][RT_BLOCK_BVH] stack words (the last rows spare write targets), then
+    // LDS: [stack_depth + 1][RT_BLOCK_BVH] stack words (the last row a spare write target), then
     // the top P.lds_nodes BVH nodes (64 B each)
-    v4f* lds_nodes = reinterpret_cast<v4f*>(smem + (P.stack_depth + RT_STACK_SPARE) * RT_BLOCK_BVH);
+    v4f* lds_nodes = reinterpret_cast<v4f*>(smem + (P.stack_depth + 1) * RT_BLOCK_BVH);
     const float4* src = reinterpret_cast<const float4*>(P.nodes);
     for (int i = threadIdx.x; i < 4 * P.lds_nodes; i += RT_BLOCK_BVH) {
       const float4 q = src[i];
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void rt_resolve_kernel(const long long* __rest
 
 static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
   return (variant & RT_VAR_BASE) == RT_VAR_FLAT ? 0
-                                                 : (size_t)(stack_depth + RT_STACK_SPARE) * RT_BLOCK_BVH * sizeof(int) + (size_t)lds_nodes * 64;
+                                                 : (size_t)(stack_depth + 1) * RT_BLOCK_BVH * sizeof(int) + (size_t)lds_nodes * 64;
 }
 
 // the kernel instantiation of a variant code (base variant | RT_VAR_TEX | RT_VAR_NOISE |

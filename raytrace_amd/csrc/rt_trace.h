@@ -55,7 +55,6 @@ inline int f2i(float f) {
 extern thread_local long long counters[4];
 }  // namespace rt_emu
 #define RT_F2I(f) rt_emu::f2i(f)
-#define RT_F2U(f) ((uint32_t)rt_emu::f2i(f))
 #define RT_COUNT(i) (++rt_emu::counters[i])
 #define RT_ANY(x) (x)  // the emulator runs one lane per wave
 #define RT_BALLOT_COUNT(x) ((x) ? 1 : 0)
@@ -64,7 +63,6 @@ extern thread_local long long counters[4];
 #define RT_FN __device__ __forceinline__
 #define RT_FN_SPEC __device__ __forceinline__
 #define RT_F2I(f) __float_as_int(f)
-#define RT_F2U(f) __float_as_uint(f)
 #define RT_COUNT(i) ((void)0)
 #define RT_ANY(x) __any(x)
 #define RT_BALLOT_COUNT(x) ((int)__popcll(__ballot(x)))
@@ -470,46 +468,29 @@ RT_FN void prep_ray(RayCtx& R) {
   prep_axis(R.o.y, R.d.y, R.idir.y, R.off0.y, R.off1.y);
   prep_axis(R.o.z, R.d.z, R.idir.z, R.off0.z, R.off1.z);
 }
-// One child box (exact float planes lo, hi) against (tmin, t_closest): the entry `nr` and exit
-// `fr`; the child is entered when nr <= fr.  tests/test_node_test.py checks on the host emulator
-// that this accepts every box the exact slab test accepts.
-RT_FN void child_slab(const RayCtx& R, f3n lo, f3n hi, float tminf, float ctf, float& nr, float& fr) {
-  const float x0 = fmaf(lo.x, R.idir.x, -R.off0.x), x1 = fmaf(hi.x, R.idir.x, -R.off1.x);
-  const float y0 = fmaf(lo.y, R.idir.y, -R.off0.y), y1 = fmaf(hi.y, R.idir.y, -R.off1.y);
-  const float z0 = fmaf(lo.z, R.idir.z, -R.off0.z), z1 = fmaf(hi.z, R.idir.z, -R.off1.z);
-  nr = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tminf));
-  fr = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), ctf)) * 1.00000095f;
-}
-// The two-box form (n0 = left x / y bounds, n1 = right x / y, n2 = left z, right z; min before
-// max), kept for the host property test of the slab arithmetic.
+// The two children's slab intervals of one BVH node (n0 = left x / y bounds, n1 = right x / y,
+// n2 = left z, right z; min before max) against (tmin, t_closest); a child is entered when its
+// near <= far.  tests/test_node_test.py checks on the host emulator that this accepts every box
+// the exact slab test accepts.
 RT_FN void node_slabs_f32(const RayCtx& R, const v4f& n0, const v4f& n1, const v4f& n2, float tminf, float ctf,
                           float& lnear, float& lfar, float& rnear, float& rfar) {
-  child_slab(R, f3n{n0.x, n0.z, n2.x}, f3n{n0.y, n0.w, n2.y}, tminf, ctf, lnear, lfar);
-  child_slab(R, f3n{n1.x, n1.z, n2.z}, f3n{n1.y, n1.w, n2.w}, tminf, ctf, rnear, rfar);
+  const float lx0 = fmaf(n0.x, R.idir.x, -R.off0.x), lx1 = fmaf(n0.y, R.idir.x, -R.off1.x);
+  const float ly0 = fmaf(n0.z, R.idir.y, -R.off0.y), ly1 = fmaf(n0.w, R.idir.y, -R.off1.y);
+  const float lz0 = fmaf(n2.x, R.idir.z, -R.off0.z), lz1 = fmaf(n2.y, R.idir.z, -R.off1.z);
+  const float rx0 = fmaf(n1.x, R.idir.x, -R.off0.x), rx1 = fmaf(n1.y, R.idir.x, -R.off1.x);
+  const float ry0 = fmaf(n1.z, R.idir.y, -R.off0.y), ry1 = fmaf(n1.w, R.idir.y, -R.off1.y);
+  const float rz0 = fmaf(n2.z, R.idir.z, -R.off0.z), rz1 = fmaf(n2.w, R.idir.z, -R.off1.z);
+  lnear = fmaxf(fmaxf(fminf(lx0, lx1), fminf(ly0, ly1)), fmaxf(fminf(lz0, lz1), tminf));
+  lfar = fminf(fminf(fmaxf(lx0, lx1), fmaxf(ly0, ly1)), fminf(fmaxf(lz0, lz1), ctf)) * 1.00000095f;
+  rnear = fmaxf(fmaxf(fminf(rx0, rx1), fminf(ry0, ry1)), fmaxf(fminf(rz0, rz1), tminf));
+  rfar = fminf(fminf(fmaxf(rx0, rx1), fmaxf(ry0, ry1)), fminf(fmaxf(rz0, rz1), ctf)) * 1.00000095f;
 }
 #else
 RT_FN void prep_ray(RayCtx& R) {
   R.idir = mk3(safe_rcp(R.d.x), safe_rcp(R.d.y), safe_rcp(R.d.z));
   R.oidir = R.o * R.idir;
 }
-struct f3n {
-  float x, y, z;
-};
-// the slab test of one child box in the kernel's precision (float kernels; the binary64 slab
-// test of the RT_NODE_F64 experiment)
-RT_FN void child_slab(const RayCtx& R, f3n lo, f3n hi, real tminf, real ctf, float& nr, float& fr) {
-  const real x0 = RFMA((real)lo.x, R.idir.x, -R.oidir.x), x1 = RFMA((real)hi.x, R.idir.x, -R.oidir.x);
-  const real y0 = RFMA((real)lo.y, R.idir.y, -R.oidir.y), y1 = RFMA((real)hi.y, R.idir.y, -R.oidir.y);
-  const real z0 = RFMA((real)lo.z, R.idir.z, -R.oidir.z), z1 = RFMA((real)hi.z, R.idir.z, -R.oidir.z);
-  const real n = RMAX(RMAX(RMIN(x0, x1), RMIN(y0, y1)), RMAX(RMIN(z0, z1), tminf));
-  const real f = RMIN(RMIN(RMAX(x0, x1), RMAX(y0, y1)), RMIN(RMAX(z0, z1), ctf));
-  // compared as floats: rounding a double pair to float keeps n <= f (monotone)
-  nr = (float)n;
-  fr = (float)f;
-}
 #endif
-// byte j of a code word as a float (v_cvt_f32_ubyte<j>)
-RT_FN float ubyte_f(uint32_t w, int j) { return (float)((w >> (8 * j)) & 255u); }
 
 // Two-level instancing (rt_internal.h DevInstance): world -> object space through the inverse of
 // the rigid placement (R^T (p - t); t is unchanged along the ray) and object -> world normals.
@@ -1102,88 +1083,103 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
       }
     }
     RT_COUNT(0);
-    // 4-wide node (rt_bvh.cpp, 64 B): (ox, oy, oz, sx) (sy, sz, qlo.x, qhi.x) (qlo.y, qhi.y, qlo.z,
-    // qhi.z) (child 0..3); child j's box planes are fma(byte j of a code word, s, o), exact floats
     v4f n0, n1, n2;
-    i4 ch;
+    int cl, cr;
     const int node = S.node;
     if (node < P.lds_nodes) {  // top levels of the surface BVH, staged in LDS per workgroup
       const v4f* nd = W.lds_nodes + 4 * node;
       n0 = nd[0];
       n1 = nd[1];
       n2 = nd[2];
-      const v4f c4 = nd[3];
-      ch = i4{RT_F2I(c4.x), RT_F2I(c4.y), RT_F2I(c4.z), RT_F2I(c4.w)};
+      cl = RT_F2I(nd[3].x);
+      cr = RT_F2I(nd[3].y);
     } else {
       cfpf nd = (cfpf)P.nodes + 16 * (size_t)node;
       n0 = ldc4f(nd);
       n1 = ldc4f(nd + 4);
       n2 = ldc4f(nd + 8);
-      const RT_CAS i4* c4 = (const RT_CAS i4*)(nd + 12);
-      ch = i4{c4->x, c4->y, c4->z, c4->w};
+      const RT_CAS i4* n3p = (const RT_CAS i4*)(nd + 12);
+      cl = n3p->x;
+      cr = n3p->y;
     }
-    const uint32_t qlx = RT_F2U(n1.z), qhx = RT_F2U(n1.w), qly = RT_F2U(n2.x), qhy = RT_F2U(n2.y),
-                   qlz = RT_F2U(n2.z), qhz = RT_F2U(n2.w);
 #if RT_NODE_F32
-    const float tminf = (float)S.tmin, ctf = (float)S.C.t;
+    float lnear, lfar, rnear, rfar;
+    node_slabs_f32(R, n0, n1, n2, (float)S.tmin, (float)S.C.t, lnear, lfar, rnear, rfar);
 #else
-    const real tminf = S.tmin, ctf = S.C.t;
-#endif
-    float key[4];
-    int ref[4] = {ch.x, ch.y, ch.z, ch.w};
-    int h = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const f3n lo{fmaf(ubyte_f(qlx, j), n0.w, n0.x), fmaf(ubyte_f(qly, j), n1.x, n0.y), fmaf(ubyte_f(qlz, j), n1.y, n0.z)};
-      const f3n hi{fmaf(ubyte_f(qhx, j), n0.w, n0.x), fmaf(ubyte_f(qhy, j), n1.x, n0.y), fmaf(ubyte_f(qhz, j), n1.y, n0.z)};
-      float nr, fr;
-      child_slab(R, lo, hi, tminf, ctf, nr, fr);
-      const bool hit = ref[j] != kDone && nr <= fr;
-      key[j] = hit ? fminf(nr, 3.0e38f) : __builtin_inff();  // entered children sort first, nearest first
-      h += hit ? 1 : 0;
-    }
-    // sort the four (entry, child) pairs: 5 compare-exchanges
-    auto cex = [&](int i, int k) {
-      const bool sw = key[k] < key[i];
-      const float ki = key[i], kk = key[k];
-      const int ri = ref[i], rk = ref[k];
-      key[i] = sw ? kk : ki;
-      key[k] = sw ? ki : kk;
-      ref[i] = sw ? rk : ri;
-      ref[k] = sw ? ri : rk;
-    };
-    cex(0, 1);
-    cex(2, 3);
-    cex(0, 2);
-    cex(1, 3);
-    cex(1, 2);
+    real lx0 = RFMA(n0.x, R.idir.x, -R.oidir.x), lx1 = RFMA(n0.y, R.idir.x, -R.oidir.x);
+    real ly0 = RFMA(n0.z, R.idir.y, -R.oidir.y), ly1 = RFMA(n0.w, R.idir.y, -R.oidir.y);
+    real lz0 = RFMA(n2.x, R.idir.z, -R.oidir.z), lz1 = RFMA(n2.y, R.idir.z, -R.oidir.z);
+    real rx0 = RFMA(n1.x, R.idir.x, -R.oidir.x), rx1 = RFMA(n1.y, R.idir.x, -R.oidir.x);
+    real ry0 = RFMA(n1.z, R.idir.y, -R.oidir.y), ry1 = RFMA(n1.w, R.idir.y, -R.oidir.y);
+    real rz0 = RFMA(n2.z, R.idir.z, -R.oidir.z), rz1 = RFMA(n2.w, R.idir.z, -R.oidir.z);
+    real lnear = RMAX(RMAX(RMIN(lx0, lx1), RMIN(ly0, ly1)), RMAX(RMIN(lz0, lz1), S.tmin));
+    real lfar = RMIN(RMIN(RMAX(lx0, lx1), RMAX(ly0, ly1)), RMIN(RMAX(lz0, lz1), S.C.t));
+    real rnear = RMAX(RMAX(RMIN(rx0, rx1), RMIN(ry0, ry1)), RMAX(RMIN(rz0, rz1), S.tmin));
+    real rfar = RMIN(RMIN(RMAX(rx0, rx1), RMAX(ry0, ry1)), RMIN(RMAX(rz0, rz1), S.C.t));
+#ifdef RT_EXP_DOUBLE_NODE  // (binary64 node test only)  // ablation: the slab tests computed twice (marginal cost of a node visit)
     {
-      // Branch-free step: the nearest entered child is next; the other h - 1 are pushed, farthest
-      // deepest (slot sp + j holds child h - 1 - j), written unconditionally to slots sp .. sp + 2
-      // (rows stack_depth .. stack_depth + 2 are spare, RT_STACK_SPARE); the stack slots a pop may
-      // need (sp - 1, sp - 2) are read every step; next node and stack pointer are selects.
+      const real e = (real)P.cam.pad;
+      real ax0 = RFMA(n0.x + e, R.idir.x, -R.oidir.x), ax1 = RFMA(n0.y + e, R.idir.x, -R.oidir.x);
+      real ay0 = RFMA(n0.z + e, R.idir.y, -R.oidir.y), ay1 = RFMA(n0.w + e, R.idir.y, -R.oidir.y);
+      real az0 = RFMA(n2.x + e, R.idir.z, -R.oidir.z), az1 = RFMA(n2.y + e, R.idir.z, -R.oidir.z);
+      real bx0 = RFMA(n1.x + e, R.idir.x, -R.oidir.x), bx1 = RFMA(n1.y + e, R.idir.x, -R.oidir.x);
+      real by0 = RFMA(n1.z + e, R.idir.y, -R.oidir.y), by1 = RFMA(n1.w + e, R.idir.y, -R.oidir.y);
+      real bz0 = RFMA(n2.z + e, R.idir.z, -R.oidir.z), bz1 = RFMA(n2.w + e, R.idir.z, -R.oidir.z);
+      lnear = RMIN(lnear, RMAX(RMAX(RMIN(ax0, ax1), RMIN(ay0, ay1)), RMAX(RMIN(az0, az1), S.tmin)));
+      lfar = RMAX(lfar, RMIN(RMIN(RMAX(ax0, ax1), RMAX(ay0, ay1)), RMIN(RMAX(az0, az1), S.C.t)));
+      rnear = RMIN(rnear, RMAX(RMAX(RMIN(bx0, bx1), RMIN(by0, by1)), RMAX(RMIN(bz0, bz1), S.tmin)));
+      rfar = RMAX(rfar, RMIN(RMIN(RMAX(bx0, bx1), RMAX(by0, by1)), RMIN(RMAX(bz0, bz1), S.C.t)));
+    }
+#endif
+#endif
+    const bool hl = lnear <= lfar, hr = rnear <= rfar;
+#ifndef RT_BRANCHY_STACK
+    {
+      // Branch-free step: the stack slots a pop may need (sp-1, sp-2) are read and the far child
+      // is written to slot sp (free; slot stack_depth is a spare row) every step, and the next
+      // node / stack pointer are selects — no divergent branches around the LDS accesses.
+      const bool both = hl && hr, one = hl != hr;
+      const bool rfirst = rnear < lnear;
+      const int nearc = both ? (rfirst ? cr : cl) : (hl ? cl : cr);
+      const int farc = rfirst ? cl : cr;
       const int sp = S.sp;
-      const int cap = P.stack_depth;
       const int top1 = stack[(sp > 0 ? sp - 1 : 0) * stride];
       const int top2 = stack[(sp > 1 ? sp - 2 : 0) * stride];
-      const int w0 = h == 4 ? ref[3] : h == 3 ? ref[2] : ref[1];
-      const int w1 = h == 4 ? ref[2] : ref[1];
-      stack[(sp < cap ? sp : cap) * stride] = w0;
-      stack[(sp < cap ? sp + 1 : cap + 1) * stride] = w1;
-      stack[(sp < cap ? sp + 2 : cap + 2) * stride] = ref[1];
-      int next = h > 0 ? ref[0] : (sp > 0 ? top1 : kDone);
-      int nsp = h > 0 ? sp + h - 1 : (sp > 0 ? sp - 1 : 0);
+      const bool room = sp < P.stack_depth;
+      stack[(room ? sp : P.stack_depth) * stride] = farc;
+      overflow |= (both && !room) ? 1 : 0;
+      int next = (both || one) ? nearc : (sp > 0 ? top1 : kDone);
+      int nsp = both ? (room ? sp + 1 : sp) : one ? sp : (sp > 0 ? sp - 1 : 0);
       if (next < 0 && next != kDone && S.leaf == 0) {  // park the first leaf, keep descending
         S.leaf = next;
-        // h >= 2: the next nearest child (the pushed top) instead; h == 1: pop; h == 0 (the
-        // leaf was popped): pop again
-        next = h >= 2 ? ref[1] : h == 1 ? (sp > 0 ? top1 : kDone) : (sp > 1 ? top2 : kDone);
-        nsp = h >= 2 ? sp + h - 2 : h == 1 ? (sp > 0 ? sp - 1 : 0) : (sp > 1 ? sp - 2 : 0);
+        const bool pushed = both && room;  // its pop is the far child just written
+        next = pushed ? farc : (both || one) ? (sp > 0 ? top1 : kDone) : (sp > 1 ? top2 : kDone);
+        nsp = pushed ? sp : (both || one) ? (sp > 0 ? sp - 1 : 0) : (sp > 1 ? sp - 2 : 0);
       }
-      overflow |= nsp > cap ? 1 : 0;  // the build bounds the pushes (rt_bvh.cpp): not reached
       S.node = next;
-      S.sp = nsp > cap ? cap : nsp;
+      S.sp = nsp;
     }
+#else
+    if (hl && hr) {
+      const bool rfirst = rnear < lnear;
+      const int nearc = rfirst ? cr : cl, farc = rfirst ? cl : cr;
+      if (S.sp < P.stack_depth) {
+        stack[S.sp * stride] = farc;
+        ++S.sp;
+      } else {
+        overflow = 1;
+      }
+      S.node = nearc;
+    } else if (hl || hr) {
+      S.node = hl ? cl : cr;
+    } else {
+      S.node = pop();
+    }
+    if (S.node < 0 && S.node != kDone && S.leaf == 0) {  // park the first leaf, keep descending
+      S.leaf = S.node;
+      S.node = pop();
+    }
+#endif
     // leave the node loop once P.leaf_exit_pct % of its lanes hold a leaf (100: all of them,
     // Aila & Laine's while-while); the rest keep their state and descend in the next round
     if (RT_BALLOT_COUNT(S.leaf != 0) * 100 >= RT_BALLOT_COUNT(true) * P.leaf_exit_pct) break;

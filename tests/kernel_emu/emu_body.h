@@ -52,7 +52,7 @@ int run_variant(const RT_NS::KernelParams& P, int variant, G& g, Cm& c, const RT
 
 void* worker(void* arg) {
   Shared* s = (Shared*)arg;
-  std::vector<int> stack(s->P->stack_depth + RT_STACK_SPARE);
+  std::vector<int> stack(s->P->stack_depth + 1);
   for (auto& c : rt_emu::counters) c = 0;
   Grab g{s};
   Commit c{s};
