@@ -67,6 +67,7 @@ struct DevArrays {
   DevInstanceT<R>* instances = nullptr;
   DevMediumT<R> media[RT_MAX_MEDIA];
   int resident_blocks = 0;  // render-kernel workgroups resident on the device (occupancy query)
+  int lds_nodes = 0;        // top surface-BVH nodes this precision's kernel stages in LDS per workgroup
   int upload(const HostArraysT<R>& H) {
     int rc;
     if ((rc = ::upload(&prims, H.prims)) || (rc = ::upload(&prim_shade, H.prim_shade)) ||
@@ -108,7 +109,6 @@ struct rt_device_scene {
   DevFlatSet flat_sets[1 + RT_MAX_MEDIA];
   int n_nodes = 0, n_prims = 0, max_depth = 0;
   int stack_depth = 1;       // LDS stack entries per lane
-  int lds_nodes = 0;         // top surface-BVH nodes staged in LDS per workgroup
   int variant = RT_VAR_FLAT;  // render-kernel variant (rt_internal.h RT_VAR_*)
   double build_ms = 0;       // host scene build (shared by every device of a multi-device scene)
   mutable double upload_ms = 0;  // host -> device copies of this device (common + precisions so far)
@@ -151,8 +151,21 @@ int ensure_precision(const rt_device_scene* s) {
     A = DevArrays<R>();
     return rc;
   }
+  A.lds_nodes = 0;
+  if ((s->variant & RT_VAR_BASE) != RT_VAR_FLAT) {
+    // stage as many top (breadth-first) surface nodes as fit beside the lanes' item sums and
+    // stacks in the workgroup's share of the CU's 160 KB LDS at the kernel's occupancy (1 KB
+    // granules; 4 waves per workgroup: one workgroup per SIMD wave slot); env RT_AMD_LDS_NODES
+    // caps it (0 disables, for experiments)
+    const int waves = std::max(1, rt_render_waves((const KernelParamsT<R>*)nullptr, s->variant));
+    const int budget = (163840 / waves / 1024) * 1024 - 1024;
+    const int used = rt_render_acc_lds((const KernelParamsT<R>*)nullptr, s->variant) +
+                     (s->stack_depth + 1) * RT_BLOCK_BVH * (int)sizeof(int);
+    A.lds_nodes = std::max(0, std::min(s->host->surface_nodes, (budget - used) / 64));
+    if (const char* e = std::getenv("RT_AMD_LDS_NODES")) A.lds_nodes = std::min(A.lds_nodes, std::max(0, atoi(e)));
+  }
   A.resident_blocks = rt_render_resident_blocks((const KernelParamsT<R>*)nullptr, s->device, s->stack_depth,
-                                                s->variant, s->lds_nodes);
+                                                s->variant, A.lds_nodes);
   if (A.resident_blocks <= 0) {
     A.release();
     A = DevArrays<R>();
@@ -196,7 +209,7 @@ int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_
   for (int k = 0; k < s->n_media; ++k) P.media[k] = A.media[k];
   for (int k = 0; k <= RT_MAX_MEDIA; ++k) P.flat_sets[k] = s->flat_sets[k];
   P.stack_depth = s->stack_depth;
-  P.lds_nodes = s->lds_nodes;
+  P.lds_nodes = A.lds_nodes;
   P.n_prims = s->n_prims;
   rt_host_plan_work(P, (long long)A.resident_blocks * rt_block_of(s->variant), (s->variant & RT_VAR_BASE) == RT_VAR_FLAT);
   P.trav_exit_pct = s->trav_exit_pct;
@@ -280,13 +293,6 @@ int upload_common(const std::shared_ptr<const HostScene>& Hp, int device, rt_dev
   s->max_depth = H.max_depth;
   s->stack_depth = H.max_depth > 1 ? H.max_depth : 1;
   s->variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex, H.n_instances > 0);
-  if ((s->variant & RT_VAR_BASE) != RT_VAR_FLAT) {
-    // stage as many top (breadth-first) surface nodes as fit beside the stacks in the per-
-    // workgroup budget; env RT_AMD_LDS_NODES caps it (0 disables, for experiments)
-    const int room = (RT_LDS_WG_BUDGET - (s->stack_depth + 1) * RT_BLOCK_BVH * (int)sizeof(int)) / 64;
-    s->lds_nodes = std::max(0, std::min(H.surface_nodes, room));
-    if (const char* e = std::getenv("RT_AMD_LDS_NODES")) s->lds_nodes = std::min(s->lds_nodes, std::max(0, atoi(e)));
-  }
   s->upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = s;
   return RT_OK;

@@ -54,9 +54,6 @@
 #ifndef RT_PREFIX_SHRINK
 #define RT_PREFIX_SHRINK 0.25 // ... and outliers whose removal shrinks the remaining box's area by this much
 #endif
-#ifndef RT_LDS_WG_BUDGET
-#define RT_LDS_WG_BUDGET 31744  // BVH kernel LDS per workgroup (stack + staged nodes): 5 per CU (32512 drops to 4)
-#endif
 #define RT_EMPTY_ROOT ((int)0x80000000)
 #ifndef RT_GRID_RESERVE
 #define RT_GRID_RESERVE 8  // render-grid workgroup slots left free for the resolve (rt_api.hip render_async)
@@ -346,6 +343,10 @@ void rt_host_encode8_thresholds(int encoding, double* thr);
 // resident workgroups of the render kernel for a given LDS stack depth (occupancy query)
 int rt_render_resident_blocks(const KernelParams*, int device, int stack_depth, int variant, int lds_nodes);
 int rt_render_resident_blocks(const KernelParams64*, int device, int stack_depth, int variant, int lds_nodes);
+int rt_render_waves(const KernelParams*, int variant);
+int rt_render_waves(const KernelParams64*, int variant);
+int rt_render_acc_lds(const KernelParams*, int variant);
+int rt_render_acc_lds(const KernelParams64*, int variant);
 int rt_launch_render(const KernelParams& p, int grid_blocks, int variant, void* stream);
 int rt_launch_render(const KernelParams64& p, int grid_blocks, int variant, void* stream);
 // accum / nanflag -> out (mean over spp, NaN where flagged)

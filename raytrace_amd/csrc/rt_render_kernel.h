@@ -5,7 +5,20 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "rt_trace.h"
+
+// Where the lanes' item sums live (rt_trace.h Acc / AccLds).  Same-box A/B against registers
+// (profiles/r3/slim): in LDS they free the VGPRs that let the FP32 BVH kernel without media run 6
+// waves per SIMD (bunny-Cornell 107.2 -> 100.6 ms) and trim the binary64 BVH kernels (bunny 162.7
+// -> 157.6, pawn+fog 643 -> 631); the flat kernels, which read their scene with scalar loads that
+// share the LDS return counter, lose 2-3.5 % (Cornell f64 6.12 -> 6.33) and the FP32 media kernel
+// 2.8 %, so those keep registers.  -DRT_ACC_IN_LDS=0 keeps registers everywhere.
+#ifndef RT_ACC_IN_LDS
+#define RT_ACC_IN_LDS 1
+#endif
+#define RT_ACC_LDS_OF(kVar, kMedia) (RT_ACC_IN_LDS && (kVar) != RT_VAR_FLAT && (RT_F64 || !(kMedia)))
 
 namespace RT_NS {
 namespace {
@@ -89,7 +102,9 @@ struct WaveGrab {
 struct AtomicCommit {
   unsigned long long* accum;
   unsigned int* nanflag;
-  __device__ __forceinline__ void operator()(int tp, const Acc& A, bool bad) const {
+  template <class AccT>
+  __device__ __forceinline__ void operator()(int tp, const AccT& acc, bool bad) const {
+    const Acc A = acc_words(acc);
 #ifdef RT_EXP_NO_COMMIT  // ablation: drop the sums (wrong image), measures the cost of the atomics
     if (A.hi[0] != 12345) return;
 #endif
@@ -133,7 +148,7 @@ struct AtomicCommit {
 #define RT_WAVES_FLAT_TEX0 7
 #endif
 #ifndef RT_WAVES_BVH_LITE
-#define RT_WAVES_BVH_LITE 5
+#define RT_WAVES_BVH_LITE 6  // 80 VGPRs once the item sums moved to LDS: bunny-Cornell 107.2 -> 100.6 ms at 6 (profiles/r3/slim)
 #endif
 // binary64: every real is a register pair, so the same code needs about twice the VGPRs; the
 // lightest instantiations (constant textures, no media, no materials beyond the diffuse ones)
@@ -175,24 +190,33 @@ void rt_render_kernel(KernelParams P) {
   WaveGrab grab{P.counter, wave * RT_POOL, RT_POOL, waves * RT_POOL, P.n_items, wave & (RT_QUEUES - 1), 0};
   AtomicCommit commit{P.accum, P.nanflag};
   int overflow;
+  // LDS: the lanes' item sums [RT_ACC_WORDS][block] (rt_trace.h AccLds), then (BVH kernels)
+  // [stack_depth + 1][RT_BLOCK_BVH] stack words (the last row a spare write target) and the top
+  // P.lds_nodes BVH nodes (64 B each)
+  using AccT = typename std::conditional<RT_ACC_LDS_OF(kVar, kMedia), AccLds, Acc>::type;
+  AccT acc;
+  int* smem_rest = smem;
+  if constexpr (RT_ACC_LDS_OF(kVar, kMedia)) {
+    acc = AccLds{reinterpret_cast<unsigned long long*>(smem) + threadIdx.x, (int)blockDim.x};
+    smem_rest = smem + 2 * RT_ACC_WORDS(real) * (int)blockDim.x;
+  }
   if constexpr (kVar == RT_VAR_FLAT) {
-    overflow =
-        lane_loop_lockstep<true, kTex, kMedia, kMats>(P, grab, commit, Trav{nullptr, 0, nullptr}, P.prims);
+    overflow = lane_loop_lockstep<true, kTex, kMedia, kMats>(P, grab, commit, Trav{nullptr, 0, nullptr}, P.prims,
+                                                              acc);
+    (void)smem_rest;
   } else {
-    // LDS: [stack_depth + 1][RT_BLOCK_BVH] stack words (the last row a spare write target), then
-    // the top P.lds_nodes BVH nodes (64 B each)
-    v4f* lds_nodes = reinterpret_cast<v4f*>(smem + (P.stack_depth + 1) * RT_BLOCK_BVH);
+    v4f* lds_nodes = reinterpret_cast<v4f*>(smem_rest + (P.stack_depth + 1) * RT_BLOCK_BVH);
     const float4* src = reinterpret_cast<const float4*>(P.nodes);
     for (int i = threadIdx.x; i < 4 * P.lds_nodes; i += RT_BLOCK_BVH) {
       const float4 q = src[i];
       lds_nodes[i] = v4f{q.x, q.y, q.z, q.w};
     }
     __syncthreads();
-    const Trav W{smem + threadIdx.x, RT_BLOCK_BVH, lds_nodes};
+    const Trav W{smem_rest + threadIdx.x, RT_BLOCK_BVH, lds_nodes};
     if constexpr (kVar == RT_VAR_BVH_LOCKSTEP)
-      overflow = lane_loop_lockstep<false, kTex, kMedia, kMats>(P, grab, commit, W, P.prims);
+      overflow = lane_loop_lockstep<false, kTex, kMedia, kMats>(P, grab, commit, W, P.prims, acc);
     else
-      overflow = lane_loop_bvh<kTex, kMedia, kMats, kInst>(P, grab, commit, W, P.prims);
+      overflow = lane_loop_bvh<kTex, kMedia, kMats, kInst>(P, grab, commit, W, P.prims, acc);
   }
   if (overflow) atomicOr(P.status, 1);
 }
@@ -217,9 +241,14 @@ __global__ __launch_bounds__(256) void rt_resolve_kernel(const long long* __rest
   }
 }
 
+static bool acc_in_lds(int variant) {
+  return RT_ACC_LDS_OF((variant & RT_VAR_BASE) == RT_VAR_FLAT ? RT_VAR_FLAT : RT_VAR_BVH, (variant & RT_VAR_MEDIA) != 0);
+}
 static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
-  return (variant & RT_VAR_BASE) == RT_VAR_FLAT ? 0
-                                                 : (size_t)(stack_depth + 1) * RT_BLOCK_BVH * sizeof(int) + (size_t)lds_nodes * 64;
+  const size_t acc = acc_in_lds(variant) ? (size_t)RT_ACC_WORDS(real) * 8 * rt_block_of(variant) : 0;
+  return acc + ((variant & RT_VAR_BASE) == RT_VAR_FLAT
+                    ? 0
+                    : (size_t)(stack_depth + 1) * RT_BLOCK_BVH * sizeof(int) + (size_t)lds_nodes * 64);
 }
 
 // the kernel instantiation of a variant code (base variant | RT_VAR_TEX | RT_VAR_NOISE |
@@ -270,6 +299,19 @@ int rt_render_resident_blocks(const KernelParamsT<RT_NS::real>*, int device, int
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return -1;
   if (per_cu < 1) per_cu = 1;
   return per_cu * cus;
+}
+
+// the render kernel's occupancy target (waves per SIMD) for a variant, and the LDS the lanes'
+// item sums take per workgroup: the host sizes the LDS node staging to what is left of the
+// workgroup's share of a CU's LDS at that occupancy (rt_api.hip ensure_precision)
+int rt_render_waves(const KernelParamsT<RT_NS::real>*, int variant) {
+  const bool flat = (variant & RT_VAR_BASE) == RT_VAR_FLAT;
+  const int tex = (variant & RT_VAR_NOISE) ? 2 : (variant & RT_VAR_TEX) ? 1 : 0;
+  const bool media = (variant & RT_VAR_MEDIA) != 0, mats = (variant & RT_VAR_MATS) != 0;
+  return RT_WAVES_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats);
+}
+int rt_render_acc_lds(const KernelParamsT<RT_NS::real>*, int variant) {
+  return RT_NS::acc_in_lds(variant) ? (int)(RT_ACC_WORDS(RT_NS::real) * 8 * rt_block_of(variant)) : 0;
 }
 
 int rt_launch_render(const KernelParamsT<RT_NS::real>& p, int grid_blocks, int variant, void* stream) {

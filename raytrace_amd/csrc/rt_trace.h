@@ -967,6 +967,51 @@ RT_FN void acc_sample(Acc& A, f3 L, bool& bad) {
   acc_add(A, 1, L.y, bad);
   acc_add(A, 2, L.z, bad);
 }
+// The item's sums in the workgroup's LDS instead of registers (the device kernels): word k of the
+// lane is w[k * stride] (word-major: a wave's 64 lanes touch consecutive 8-B words, no bank
+// conflicts).  A sample adds its words with LDS atomics (ds_add_u64, no return); the words are
+// read once per item, at its commit.  Frees RT_ACC_WORDS x 2 VGPRs of state that is touched once
+// per sample but live across the whole lane loop.
+struct AccLds {
+  unsigned long long* w;
+  int stride;
+};
+RT_FN void acc_clear(AccLds& A) {
+#pragma unroll
+  for (int k = 0; k < RT_ACC_WORDS(real); ++k) A.w[k * A.stride] = 0ull;
+}
+RT_FN void lds_add(unsigned long long* p, unsigned long long v) {
+#ifdef RT_HOST_EMU
+  *p += v;
+#else
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+}
+RT_FN void acc_sample(AccLds& A, f3 L, bool& bad) {
+  Acc t;
+  acc_clear(t);
+  acc_sample(t, L, bad);
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+    if (t.hi[c]) lds_add(A.w + c * A.stride, (unsigned long long)t.hi[c]);
+#if RT_F64
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+    if (t.lo[c]) lds_add(A.w + (3 + c) * A.stride, t.lo[c]);
+#endif
+}
+// the sums of an accumulator (commit)
+RT_FN Acc acc_words(const Acc& A) { return A; }
+RT_FN Acc acc_words(const AccLds& A) {
+  Acc t;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) t.hi[c] = (long long)A.w[c * A.stride];
+#if RT_F64
+#pragma unroll
+  for (int c = 0; c < 3; ++c) t.lo[c] = A.w[(3 + c) * A.stride];
+#endif
+  return t;
+}
 
 // Diagnostic build only (make exp DEFS=-DRT_PHASE_PROF, tools/phase_prof.py): per-wave shader
 // clocks and lane counts by phase of lane_loop_bvh and trav_round, summed over the launch into
@@ -1263,7 +1308,13 @@ RT_FN_SPEC void closest<false>(const KernelParams& P, cfp prims, int root, int s
 
 // ------------------------------------------------------------------ per-path pieces
 // Ray.hs:157-172, 229: pixel jitter, time, defocus-disk point -> primary ray
-RT_FN void camera_ray(const KernelParams& P, uint32_t pix, int sample, int px, int gy, RayCtx& R) {
+RT_FN uint32_t fast_div(uint32_t n, const FastDiv& f) {
+  if (f.d == 1u) return n;  // uniform
+  const uint32_t t = (uint32_t)(((uint64_t)n * f.m) >> 32);
+  return (t + ((n - t) >> 1)) >> f.s;
+}
+RT_FN void camera_ray(const KernelParams& P, uint32_t pix, int sample, RayCtx& R) {
+  const int gy = (int)fast_div(pix, P.div_width), px = (int)pix - gy * P.cam.width;
 #ifdef RT_EXP_CHEAP_CAMERA  // ablation (wrong image): measures the camera block's Philox cost
   u4 w0 = u4{pix * 0x9E3779B9u + (uint32_t)sample, pix ^ ((uint32_t)sample * 0x85EBCA6Bu), 0u, 0u};
 #else
@@ -1483,36 +1534,31 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
 
 // Work item -> pixel / sample range (items are claimed in pixel order, chunk index slowest).
 struct ItemCtx {
-  int item, tp, px, gy, sample, s_end;
-  uint32_t pix;
+  int tp;  // tile pixel (-1: no item yet)
+  int sample, s_end;
+  uint32_t pix;  // global pixel gy * width + px (the column and row follow from it at camera_ray)
 };
-RT_FN uint32_t fast_div(uint32_t n, const FastDiv& f) {
-  if (f.d == 1u) return n;  // uniform
-  const uint32_t t = (uint32_t)(((uint64_t)n * f.m) >> 32);
-  return (t + ((n - t) >> 1)) >> f.s;
-}
 // kTwoSizes: the item may be big (flat kernel only: the BVH kernels run one item size, rt_build.cpp
 // rt_host_plan_work, so their register allocation does not carry the decode)
 template <bool kTwoSizes>
 RT_FN bool open_item(const KernelParams& P, int item, ItemCtx& I) {
   const int W = P.cam.width, tile_pixels = P.tile_rows * W;
-  I.item = item;
   // item, tile pixel and row are non-negative: exact multiply-shift division by the launch
   // constants instead of the ~20-instruction signed integer division sequences
   const int k = (int)fast_div((uint32_t)item, P.div_tile);
   I.tp = item - k * tile_pixels;
   const int tr = (int)fast_div((uint32_t)I.tp, P.div_width);
-  I.px = I.tp - tr * W;
+  const int px = I.tp - tr * W;
   const int tb = (int)fast_div((uint32_t)tr, P.div_block);
-  I.gy = (tb * P.n_shards + P.shard) * P.row_block + (tr - tb * P.row_block);
-  I.pix = (uint32_t)(I.gy * W + I.px);
+  const int gy = (tb * P.n_shards + P.shard) * P.row_block + (tr - tb * P.row_block);
+  I.pix = (uint32_t)(gy * W + px);
   // chunks k < n_big_chunks are big (samples [k big_chunk, (k + 1) big_chunk)), the rest small
   // (from n_big_chunks big_chunk = small_base + n_big_chunks chunk on)
   const bool big = kTwoSizes && k < P.n_big_chunks;
   const int chunk = big ? P.big_chunk : P.chunk;
   I.sample = (big ? 0 : kTwoSizes ? P.small_base : 0) + k * chunk;
   I.s_end = I.sample + chunk < P.cam.spp ? I.sample + chunk : P.cam.spp;
-  if (I.gy >= P.cam.height || P.cam.max_depth <= 0) I.s_end = I.sample;  // padding row / black image
+  if (gy >= P.cam.height || P.cam.max_depth <= 0) I.s_end = I.sample;  // padding row / black image
   return I.sample < I.s_end;
 }
 
@@ -1521,31 +1567,33 @@ RT_FN bool open_item(const KernelParams& P, int item, ItemCtx& I) {
 // sums.  One segment per iteration, all of its queries run by the whole wave together: the flat
 // kernel (every lane tests the same primitives), and the lockstep BVH variant kept for
 // experiments (RT_VAR_BVH_LOCKSTEP; BVH scenes, media or not, default to lane_loop_bvh).
-template <bool kFlat, int kTex, bool kMedia, bool kMats, class Grab, class Commit>
+template <bool kFlat, int kTex, bool kMedia, bool kMats, class Grab, class Commit, class AccT>
 RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW,
-                             const real* prims_) {
+                             const real* prims_, AccT& acc) {
   const cfp prims = cf(prims_);
   int overflow = 0;
-  ItemCtx I{-1, 0, 0, 0, 0, 0, 0u};
+  ItemCtx I{-1, 0, 0, 0u};
   int seg = 0;
-  Acc acc;
   acc_clear(acc);
   bool bad = false;
   bool alive = false;
-  f3 L = mk3(RL(0.), RL(0.), RL(0.)), T = mk3(RL(1.), RL(1.), RL(1.));
+  // T: the path throughput.  The radiance needs no register across iterations: only the event
+  // that ends a path emits (lightSource absorbs, Material.hs:41-44; a miss returns the background,
+  // Ray.hs:179), so a sample's radiance is that one term, formed in `shade` and summed at once.
+  f3 T = mk3(RL(1.), RL(1.), RL(1.));
   RayCtx R;
-  R.o = R.d = L;
+  R.o = R.d = mk3(RL(0.), RL(0.), RL(0.));
 #if RT_NODE_F32
   R.idir = R.off0 = R.off1 = f3n{0.f, 0.f, 0.f};
 #else
-  R.idir = R.oidir = L;
+  R.idir = R.oidir = R.o;
 #endif
   R.time = RL(0.0);
   R.self_gid = -1;
   R.self_inst = -1;
   for (;;) {
     const bool need = !alive && I.sample >= I.s_end;
-    if (need && I.item >= 0) commit(I.tp, acc, bad);
+    if (need && I.tp >= 0) commit(I.tp, acc, bad);
     const int got = grab(need);
     if (need) {
       if (got >= P.n_items) break;
@@ -1554,8 +1602,7 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
       if (!open_item<kFlat>(P, got, I)) continue;
     }
     if (!alive) {
-      camera_ray(P, I.pix, I.sample, I.px, I.gy, R);
-      L = mk3(RL(0.), RL(0.), RL(0.));
+      camera_ray(P, I.pix, I.sample, R);
       T = mk3(RL(1.), RL(1.), RL(1.));
       seg = 0;
       alive = true;
@@ -1596,6 +1643,7 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
       }
       medium_event(P, m, I.pix, I.sample, seg, lo, hi, tbest, hit_medium);
     }
+    f3 L = mk3(RL(0.), RL(0.), RL(0.));
     if (shade<kTex, kMats>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T)) {
       RT_HOOK_SAMPLE(I.pix, I.sample, L);
       acc_sample(acc, L, bad);
@@ -1617,24 +1665,27 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
 // entering it, the second (Geometry.hs:306-328) — each starting inside the traversal loop as
 // soon as the previous one finishes.
 enum : int { ST_NEED_ITEM = 0, ST_NEED_SAMPLE = 1, ST_START_SEG = 2, ST_TRACE = 3, ST_SHADE = 4 };
-template <int kTex, bool kMedia, bool kMats, bool kInst, class Grab, class Commit>
-RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW, const real* prims_) {
+template <int kTex, bool kMedia, bool kMats, bool kInst, class Grab, class Commit, class AccT>
+RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW, const real* prims_,
+                        AccT& acc) {
   const cfp prims = cf(prims_);
   const int n_media = kMedia ? P.n_media : 0;  // media code only in the kMedia instantiations
   int overflow = 0;
-  ItemCtx I{-1, 0, 0, 0, 0, 0, 0u};
+  ItemCtx I{-1, 0, 0, 0u};
   int seg = 0;
-  Acc acc;
   acc_clear(acc);
   bool bad = false;
   int state = ST_NEED_ITEM;
-  f3 L = mk3(RL(0.), RL(0.), RL(0.)), T = mk3(RL(1.), RL(1.), RL(1.));
+  // T: the path throughput.  The radiance needs no register across iterations: only the event
+  // that ends a path emits (lightSource absorbs, Material.hs:41-44; a miss returns the background,
+  // Ray.hs:179), so a sample's radiance is that one term, formed in `shade` and summed at once.
+  f3 T = mk3(RL(1.), RL(1.), RL(1.));
   RayCtx R;
-  R.o = R.d = L;
+  R.o = R.d = mk3(RL(0.), RL(0.), RL(0.));
 #if RT_NODE_F32
   R.idir = R.off0 = R.off1 = f3n{0.f, 0.f, 0.f};
 #else
-  R.idir = R.oidir = L;
+  R.idir = R.oidir = R.o;
 #endif
   R.time = RL(0.0);
   R.self_gid = -1;
@@ -1650,7 +1701,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
     const bool need = state == ST_NEED_ITEM;
     RT_PROF_ADD(PF_ITERS, 1);
     RT_PROF_ADD(PF_FRONT_LANES, RT_BALLOT_COUNT(state != ST_TRACE));
-    if (need && I.item >= 0) commit(I.tp, acc, bad);
+    if (need && I.tp >= 0) commit(I.tp, acc, bad);
     const int got = grab(need);
     if (need) {
       if (got >= P.n_items) break;
@@ -1659,8 +1710,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
       state = open_item<false>(P, got, I) ? ST_NEED_SAMPLE : ST_NEED_ITEM;
     }
     if (state == ST_NEED_SAMPLE) {
-      camera_ray(P, I.pix, I.sample, I.px, I.gy, R);
-      L = mk3(RL(0.), RL(0.), RL(0.));
+      camera_ray(P, I.pix, I.sample, R);
       T = mk3(RL(1.), RL(1.), RL(1.));
       seg = 0;
       state = ST_START_SEG;
@@ -1741,6 +1791,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
     RT_PROF_ADD(PF_SHADING, RT_BALLOT_COUNT(state == ST_SHADE));
     // ---- shade the segments whose queries are complete
     if (state == ST_SHADE) {
+      f3 L = mk3(RL(0.), RL(0.), RL(0.));
       if (shade<kTex, kMats, kInst>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T, best_inst)) {
         RT_HOOK_SAMPLE(I.pix, I.sample, L);
         acc_sample(acc, L, bad);

@@ -17,7 +17,9 @@ struct Grab {
 };
 struct Commit {
   Shared* s;
-  void operator()(int tp, const RT_NS::Acc& A, bool bad) {
+  template <class AccT>
+  void operator()(int tp, const AccT& acc, bool bad) {
+    const RT_NS::Acc A = RT_NS::acc_words(acc);
     const size_t w = RT_ACC_WORDS(RT_NS::real);
     for (int c = 0; c < 3; ++c) (*s->accum)[w * (size_t)tp + c] += A.hi[c];
 #if RT_F64
@@ -29,11 +31,15 @@ struct Commit {
 
 template <int kTex, bool kMedia, bool kMats, class G, class Cm>
 int run_loop(const RT_NS::KernelParams& P, int variant, G& g, Cm& c, const RT_NS::Trav& W) {
-  if (variant & RT_VAR_INST) return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, true>(P, g, c, W, P.prims);
+  // the item sums through the device kernels' LDS accumulator (one lane: stride 1)
+  unsigned long long words[6] = {0, 0, 0, 0, 0, 0};
+  RT_NS::AccLds acc{words, 1};
+  if (variant & RT_VAR_INST) return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, true>(P, g, c, W, P.prims, acc);
   switch (variant & RT_VAR_BASE) {
-    case RT_VAR_FLAT: return RT_NS::lane_loop_lockstep<true, kTex, kMedia, kMats>(P, g, c, W, P.prims);
-    case RT_VAR_BVH_LOCKSTEP: return RT_NS::lane_loop_lockstep<false, kTex, kMedia, kMats>(P, g, c, W, P.prims);
-    default: return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, false>(P, g, c, W, P.prims);
+    case RT_VAR_FLAT: return RT_NS::lane_loop_lockstep<true, kTex, kMedia, kMats>(P, g, c, W, P.prims, acc);
+    case RT_VAR_BVH_LOCKSTEP:
+      return RT_NS::lane_loop_lockstep<false, kTex, kMedia, kMats>(P, g, c, W, P.prims, acc);
+    default: return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, false>(P, g, c, W, P.prims, acc);
   }
 }
 template <int kTex, class G, class Cm>
