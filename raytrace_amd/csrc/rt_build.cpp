@@ -967,11 +967,13 @@ void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_s
     int c = std::atoi(env);
     if (c > 0) chunk = c;
   }
-  // Big items for the bulk of the samples, small ones for the tail: the first samples of every
-  // pixel go in 16-sample items (a quarter of the commit atomics, 7 % of the binary64 Cornell
-  // kernel), the last T in `chunk`-sample items, T such that the tail alone still gives every
-  // resident lane RT_TAIL_ITEMS_* items (the queue's end stays as short as with small items only).
-  int big = 16, n_big = 0;
+  // Big items for the bulk of the samples, small ones for the tail: the last T samples of every
+  // pixel go in `chunk`-sample items, T such that the tail alone still gives every resident lane
+  // RT_TAIL_ITEMS_* items (the queue's end stays as short as with small items only), and the
+  // first spp - T in as few items of at most RT_BIG_CHUNK_MAX samples as cover them exactly
+  // (Cornell binary64 at 1 GPU: 16 items per pixel instead of 23 with fixed 16-sample items, and
+  // as many fewer commit atomics; measured equal in time, profiles/r3/items).
+  int big = RT_BIG_CHUNK_MAX, n_big = 0;
   if (const char* env = std::getenv("RT_AMD_BIG_CHUNK")) big = std::max(1, std::atoi(env));
   int tail_items = sizeof(R) == 8 ? RT_TAIL_ITEMS_F64 : RT_TAIL_ITEMS_F32;
   if (const char* env = std::getenv("RT_AMD_TAIL_ITEMS")) tail_items = std::atoi(env);
@@ -979,7 +981,13 @@ void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_s
     long long t = ((long long)tail_items * chunk * resident_lanes + tile_pixels - 1) / tile_pixels;
     if (const char* env = std::getenv("RT_AMD_TAIL_SAMPLES")) t = std::max(0, std::atoi(env));  // tests
     const long long tail = ((t + chunk - 1) / chunk) * chunk;  // tail samples, a multiple of chunk
-    if (tail < spp) n_big = (int)((spp - tail) / big);
+    if (tail < spp) {
+      const long long bulk = spp - tail;
+      n_big = (int)((bulk + big - 1) / big);
+      big = (int)((bulk + n_big - 1) / n_big);  // <= the maximum; n_big items cover the bulk
+      big = std::min(big, spp / n_big);          // the small items cover [n_big big, spp)
+      if (big <= chunk) n_big = 0;
+    }
   }
   const int n_chunks = (spp - n_big * big + chunk - 1) / chunk;
   long long items = (long long)(n_big + n_chunks) * tile_pixels;

@@ -37,6 +37,9 @@
 // small items per resident lane kept for the queue tail (rt_build.cpp rt_host_plan_work; 0: one
 // item size).  Cornell 600x600x200, same box (profiles/r2/items/): binary64 6.77 -> 6.63 ms at
 // 16 (8: 6.69, 32: 6.64, 64: 6.78); FP32 3.50 -> 3.46 at 32 (16: 3.49); 8-GPU shares unchanged
+#ifndef RT_BIG_CHUNK_MAX
+#define RT_BIG_CHUNK_MAX 48  // samples per big work item at most (rt_build.cpp rt_host_plan_work)
+#endif
 #ifndef RT_TAIL_ITEMS_F64
 #define RT_TAIL_ITEMS_F64 16
 #endif
