@@ -227,9 +227,10 @@ int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_
   P.nanflag = (unsigned int*)(ws + off_flag);
   P.counter = (int*)(ws + off_ctr);
   rc = RT_OK;
-  // The persistent grid leaves RT_GRID_RESERVE workgroup slots free (one per XCD): when a caller
-  // overlaps frames on two streams, the next frame's grid then cannot take every slot, and this
-  // frame's resolve runs as soon as its render ends instead of queueing behind the next render.
+  // The persistent grid can leave RT_GRID_RESERVE workgroup slots free, so that with frames
+  // overlapped on two streams this frame's resolve starts as soon as its render ends.  Measured
+  // (profiles/r3/iso): with 8 free slots the FP32 resolve still takes 3.1 ms, starved by the next
+  // frame's grid; binary64's runs in 23 us either way (its kernel leaves VGPRs free) — so 0.
   int reserve = A.resident_blocks > 16 * RT_GRID_RESERVE ? RT_GRID_RESERVE : 0;
   if (const char* e = std::getenv("RT_AMD_GRID_RESERVE")) reserve = std::max(0, std::min(A.resident_blocks - 1, atoi(e)));
   if (rt_launch_render(P, A.resident_blocks - reserve, s->variant, hip_stream) || rt_launch_resolve(P, hip_stream))

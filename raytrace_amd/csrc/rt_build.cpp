@@ -864,6 +864,9 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
   if (!(cs->aspect_ratio > 0)) return fail(err, RT_E_INVALID, "aspect ratio must be positive");
   int h = rt_host_image_height(cs);
   if (h <= 0) return fail(err, RT_E_INVALID, "image height %d must be positive", h);
+  // the kernels carry a pixel's column and row in 16 bits each (rt_trace.h ItemCtx)
+  if (cs->image_width > 65535 || h > 65535)
+    return fail(err, RT_E_UNSUPPORTED, "image %dx%d exceeds 65535 x 65535", cs->image_width, h);
   if (cs->background_kind != RT_BG_CONST && cs->background_kind != RT_BG_LERP_Y)
     return fail(err, RT_E_UNSUPPORTED, "background kind %d", cs->background_kind);
   if (cs->n_redirect_targets < 0 || cs->n_redirect_targets > RT_MAX_TARGETS)
@@ -971,8 +974,8 @@ void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_s
   // pixel go in `chunk`-sample items, T such that the tail alone still gives every resident lane
   // RT_TAIL_ITEMS_* items (the queue's end stays as short as with small items only), and the
   // first spp - T in as few items of at most RT_BIG_CHUNK_MAX samples as cover them exactly
-  // (Cornell binary64 at 1 GPU: 16 items per pixel instead of 23 with fixed 16-sample items, and
-  // as many fewer commit atomics; measured equal in time, profiles/r3/items).
+  // (at most 48: Cornell binary64 at 1 GPU would take 16 items per pixel instead of 23 and as many
+  // fewer commit atomics, but runs 1.5 % slower (6.19 vs 6.10 ms, profiles/r3/iso), so 16).
   int big = RT_BIG_CHUNK_MAX, n_big = 0;
   if (const char* env = std::getenv("RT_AMD_BIG_CHUNK")) big = std::max(1, std::atoi(env));
   int tail_items = sizeof(R) == 8 ? RT_TAIL_ITEMS_F64 : RT_TAIL_ITEMS_F32;

@@ -38,7 +38,7 @@
 // item size).  Cornell 600x600x200, same box (profiles/r2/items/): binary64 6.77 -> 6.63 ms at
 // 16 (8: 6.69, 32: 6.64, 64: 6.78); FP32 3.50 -> 3.46 at 32 (16: 3.49); 8-GPU shares unchanged
 #ifndef RT_BIG_CHUNK_MAX
-#define RT_BIG_CHUNK_MAX 48  // samples per big work item at most (rt_build.cpp rt_host_plan_work)
+#define RT_BIG_CHUNK_MAX 16  // samples per big work item at most (rt_build.cpp rt_host_plan_work; 38-48: Cornell f64 +1.5 %)
 #endif
 #ifndef RT_TAIL_ITEMS_F64
 #define RT_TAIL_ITEMS_F64 16
@@ -59,7 +59,7 @@
 #endif
 #define RT_EMPTY_ROOT ((int)0x80000000)
 #ifndef RT_GRID_RESERVE
-#define RT_GRID_RESERVE 8  // render-grid workgroup slots left free for the resolve (rt_api.hip render_async)
+#define RT_GRID_RESERVE 0  // render-grid workgroup slots left free for the resolve (rt_api.hip render_async; 8 measured no help)
 #endif
 // Two-level instancing: a BVH child RT_INST_FLAG | k enters instance k (the ray goes to object
 // space, the object's BVH is traversed); RT_INST_EXIT, pushed on entry, returns to world space.

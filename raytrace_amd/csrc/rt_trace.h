@@ -1313,8 +1313,17 @@ RT_FN uint32_t fast_div(uint32_t n, const FastDiv& f) {
   const uint32_t t = (uint32_t)(((uint64_t)n * f.m) >> 32);
   return (t + ((n - t) >> 1)) >> f.s;
 }
-RT_FN void camera_ray(const KernelParams& P, uint32_t pix, int sample, RayCtx& R) {
-  const int gy = (int)fast_div(pix, P.div_width), px = (int)pix - gy * P.cam.width;
+// pxgy: the pixel's gy << 16 | px (the flat kernel keeps it from open_item), or ~0u: derived from
+// pix here (the register-bound BVH kernels, for which a persistent word costs more than a division)
+RT_FN void camera_ray(const KernelParams& P, uint32_t pix, int sample, uint32_t pxgy, RayCtx& R) {
+  int gy, px;
+  if (pxgy == ~0u) {
+    gy = (int)fast_div(pix, P.div_width);
+    px = (int)pix - gy * P.cam.width;
+  } else {
+    gy = (int)(pxgy >> 16);
+    px = (int)(pxgy & 0xffffu);
+  }
 #ifdef RT_EXP_CHEAP_CAMERA  // ablation (wrong image): measures the camera block's Philox cost
   u4 w0 = u4{pix * 0x9E3779B9u + (uint32_t)sample, pix ^ ((uint32_t)sample * 0x85EBCA6Bu), 0u, 0u};
 #else
@@ -1536,7 +1545,8 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
 struct ItemCtx {
   int tp;  // tile pixel (-1: no item yet)
   int sample, s_end;
-  uint32_t pix;  // global pixel gy * width + px (the column and row follow from it at camera_ray)
+  uint32_t pix;   // global pixel gy * width + px
+  uint32_t pxgy;  // gy << 16 | px (rt_build.cpp limits images to 65535 x 65535)
 };
 // kTwoSizes: the item may be big (flat kernel only: the BVH kernels run one item size, rt_build.cpp
 // rt_host_plan_work, so their register allocation does not carry the decode)
@@ -1552,6 +1562,7 @@ RT_FN bool open_item(const KernelParams& P, int item, ItemCtx& I) {
   const int tb = (int)fast_div((uint32_t)tr, P.div_block);
   const int gy = (tb * P.n_shards + P.shard) * P.row_block + (tr - tb * P.row_block);
   I.pix = (uint32_t)(gy * W + px);
+  I.pxgy = (uint32_t)gy << 16 | (uint32_t)px;
   // chunks k < n_big_chunks are big (samples [k big_chunk, (k + 1) big_chunk)), the rest small
   // (from n_big_chunks big_chunk = small_base + n_big_chunks chunk on)
   const bool big = kTwoSizes && k < P.n_big_chunks;
@@ -1572,17 +1583,14 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
                              const real* prims_, AccT& acc) {
   const cfp prims = cf(prims_);
   int overflow = 0;
-  ItemCtx I{-1, 0, 0, 0u};
+  ItemCtx I{-1, 0, 0, 0u, 0u};
   int seg = 0;
   acc_clear(acc);
   bool bad = false;
   bool alive = false;
-  // T: the path throughput.  The radiance needs no register across iterations: only the event
-  // that ends a path emits (lightSource absorbs, Material.hs:41-44; a miss returns the background,
-  // Ray.hs:179), so a sample's radiance is that one term, formed in `shade` and summed at once.
-  f3 T = mk3(RL(1.), RL(1.), RL(1.));
+  f3 L = mk3(RL(0.), RL(0.), RL(0.)), T = mk3(RL(1.), RL(1.), RL(1.));
   RayCtx R;
-  R.o = R.d = mk3(RL(0.), RL(0.), RL(0.));
+  R.o = R.d = L;
 #if RT_NODE_F32
   R.idir = R.off0 = R.off1 = f3n{0.f, 0.f, 0.f};
 #else
@@ -1602,7 +1610,8 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
       if (!open_item<kFlat>(P, got, I)) continue;
     }
     if (!alive) {
-      camera_ray(P, I.pix, I.sample, R);
+      camera_ray(P, I.pix, I.sample, I.pxgy, R);
+      L = mk3(RL(0.), RL(0.), RL(0.));
       T = mk3(RL(1.), RL(1.), RL(1.));
       seg = 0;
       alive = true;
@@ -1643,7 +1652,6 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
       }
       medium_event(P, m, I.pix, I.sample, seg, lo, hi, tbest, hit_medium);
     }
-    f3 L = mk3(RL(0.), RL(0.), RL(0.));
     if (shade<kTex, kMats>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T)) {
       RT_HOOK_SAMPLE(I.pix, I.sample, L);
       acc_sample(acc, L, bad);
@@ -1671,7 +1679,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
   const cfp prims = cf(prims_);
   const int n_media = kMedia ? P.n_media : 0;  // media code only in the kMedia instantiations
   int overflow = 0;
-  ItemCtx I{-1, 0, 0, 0u};
+  ItemCtx I{-1, 0, 0, 0u, 0u};
   int seg = 0;
   acc_clear(acc);
   bool bad = false;
@@ -1710,7 +1718,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
       state = open_item<false>(P, got, I) ? ST_NEED_SAMPLE : ST_NEED_ITEM;
     }
     if (state == ST_NEED_SAMPLE) {
-      camera_ray(P, I.pix, I.sample, R);
+      camera_ray(P, I.pix, I.sample, ~0u, R);
       T = mk3(RL(1.), RL(1.), RL(1.));
       seg = 0;
       state = ST_START_SEG;
