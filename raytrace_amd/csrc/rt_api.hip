@@ -159,13 +159,13 @@ int ensure_precision(const rt_device_scene* s) {
     // caps it (0 disables, for experiments)
     const int waves = std::max(1, rt_render_waves((const KernelParamsT<R>*)nullptr, s->variant));
     const int budget = (163840 / waves / 1024) * 1024 - 1024;
-    const int used = rt_render_acc_lds((const KernelParamsT<R>*)nullptr, s->variant, s->n_media) +
+    const int used = rt_render_acc_lds((const KernelParamsT<R>*)nullptr, s->variant) +
                      (s->stack_depth + 1) * RT_BLOCK_BVH * (int)sizeof(int);
     A.lds_nodes = std::max(0, std::min(s->host->surface_nodes, (budget - used) / 64));
     if (const char* e = std::getenv("RT_AMD_LDS_NODES")) A.lds_nodes = std::min(A.lds_nodes, std::max(0, atoi(e)));
   }
   A.resident_blocks = rt_render_resident_blocks((const KernelParamsT<R>*)nullptr, s->device, s->stack_depth,
-                                                s->variant, A.lds_nodes, s->n_media);
+                                                s->variant, A.lds_nodes);
   if (A.resident_blocks <= 0) {
     A.release();
     A = DevArrays<R>();

@@ -344,13 +344,12 @@ void rt_host_encode8_thresholds(int encoding, double* thr);
 
 // rt_kernel.hip / rt_kernel64.hip (device launchers)
 // resident workgroups of the render kernel for a given LDS stack depth (occupancy query)
-int rt_render_resident_blocks(const KernelParams*, int device, int stack_depth, int variant, int lds_nodes, int n_media);
-int rt_render_resident_blocks(const KernelParams64*, int device, int stack_depth, int variant, int lds_nodes,
-                              int n_media);
+int rt_render_resident_blocks(const KernelParams*, int device, int stack_depth, int variant, int lds_nodes);
+int rt_render_resident_blocks(const KernelParams64*, int device, int stack_depth, int variant, int lds_nodes);
 int rt_render_waves(const KernelParams*, int variant);
 int rt_render_waves(const KernelParams64*, int variant);
-int rt_render_acc_lds(const KernelParams*, int variant, int n_media);
-int rt_render_acc_lds(const KernelParams64*, int variant, int n_media);
+int rt_render_acc_lds(const KernelParams*, int variant);
+int rt_render_acc_lds(const KernelParams64*, int variant);
 int rt_launch_render(const KernelParams& p, int grid_blocks, int variant, void* stream);
 int rt_launch_render(const KernelParams64& p, int grid_blocks, int variant, void* stream);
 // accum / nanflag -> out (mean over spp, NaN where flagged)

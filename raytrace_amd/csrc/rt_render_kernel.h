@@ -205,9 +205,6 @@ void rt_render_kernel(KernelParams P) {
                                                               acc);
     (void)smem_rest;
   } else {
-    // the BVH kernels with media: the lanes' deferred media events [2 n_media][block] reals
-    real* pend = reinterpret_cast<real*>(smem_rest) + threadIdx.x;
-    if constexpr (kMedia) smem_rest += (int)(sizeof(real) / sizeof(int)) * 2 * P.n_media * RT_BLOCK_BVH;
     v4f* lds_nodes = reinterpret_cast<v4f*>(smem_rest + (P.stack_depth + 1) * RT_BLOCK_BVH);
     const float4* src = reinterpret_cast<const float4*>(P.nodes);
     for (int i = threadIdx.x; i < 4 * P.lds_nodes; i += RT_BLOCK_BVH) {
@@ -219,7 +216,7 @@ void rt_render_kernel(KernelParams P) {
     if constexpr (kVar == RT_VAR_BVH_LOCKSTEP)
       overflow = lane_loop_lockstep<false, kTex, kMedia, kMats>(P, grab, commit, W, P.prims, acc);
     else
-      overflow = lane_loop_bvh<kTex, kMedia, kMats, kInst>(P, grab, commit, W, P.prims, acc, pend, RT_BLOCK_BVH);
+      overflow = lane_loop_bvh<kTex, kMedia, kMats, kInst>(P, grab, commit, W, P.prims, acc);
   }
   if (overflow) atomicOr(P.status, 1);
 }
@@ -247,11 +244,11 @@ __global__ __launch_bounds__(256) void rt_resolve_kernel(const long long* __rest
 static bool acc_in_lds(int variant) {
   return RT_ACC_LDS_OF((variant & RT_VAR_BASE) == RT_VAR_FLAT ? RT_VAR_FLAT : RT_VAR_BVH, (variant & RT_VAR_MEDIA) != 0);
 }
-static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes, int n_media) {
+static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
   const size_t acc = acc_in_lds(variant) ? (size_t)RT_ACC_WORDS(real) * 8 * rt_block_of(variant) : 0;
-  if ((variant & RT_VAR_BASE) == RT_VAR_FLAT) return acc;
-  const size_t pend = (variant & RT_VAR_MEDIA) ? (size_t)2 * n_media * sizeof(real) * RT_BLOCK_BVH : 0;
-  return acc + pend + (size_t)(stack_depth + 1) * RT_BLOCK_BVH * sizeof(int) + (size_t)lds_nodes * 64;
+  return acc + ((variant & RT_VAR_BASE) == RT_VAR_FLAT
+                    ? 0
+                    : (size_t)(stack_depth + 1) * RT_BLOCK_BVH * sizeof(int) + (size_t)lds_nodes * 64);
 }
 
 // the kernel instantiation of a variant code (base variant | RT_VAR_TEX | RT_VAR_NOISE |
@@ -290,10 +287,10 @@ static render_fn render_kernel_of(int variant) {
 }  // namespace RT_NS
 
 int rt_render_resident_blocks(const KernelParamsT<RT_NS::real>*, int device, int stack_depth, int variant,
-                              int lds_nodes, int n_media) {
+                              int lds_nodes) {
   using namespace RT_NS;
   int per_cu = 0, cus = 0;
-  size_t lds = render_lds_bytes(stack_depth, variant, lds_nodes, n_media);
+  size_t lds = render_lds_bytes(stack_depth, variant, lds_nodes);
   if (lds > 65536 && hipFuncSetAttribute((const void*)render_kernel_of(variant),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -1;
@@ -305,18 +302,16 @@ int rt_render_resident_blocks(const KernelParamsT<RT_NS::real>*, int device, int
 }
 
 // the render kernel's occupancy target (waves per SIMD) for a variant, and the LDS the lanes'
-// item sums and deferred media events take per workgroup: the host sizes the LDS node staging to
-// what is left of the workgroup's share of a CU's LDS at that occupancy (rt_api.hip
-// ensure_precision)
+// item sums take per workgroup: the host sizes the LDS node staging to what is left of the
+// workgroup's share of a CU's LDS at that occupancy (rt_api.hip ensure_precision)
 int rt_render_waves(const KernelParamsT<RT_NS::real>*, int variant) {
   const bool flat = (variant & RT_VAR_BASE) == RT_VAR_FLAT;
   const int tex = (variant & RT_VAR_NOISE) ? 2 : (variant & RT_VAR_TEX) ? 1 : 0;
   const bool media = (variant & RT_VAR_MEDIA) != 0, mats = (variant & RT_VAR_MATS) != 0;
   return RT_WAVES_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats);
 }
-int rt_render_acc_lds(const KernelParamsT<RT_NS::real>*, int variant, int n_media) {
-  using namespace RT_NS;
-  return (int)render_lds_bytes(0, variant, 0, n_media) - ((variant & RT_VAR_BASE) == RT_VAR_FLAT ? 0 : RT_BLOCK_BVH * (int)sizeof(int));
+int rt_render_acc_lds(const KernelParamsT<RT_NS::real>*, int variant) {
+  return RT_NS::acc_in_lds(variant) ? (int)(RT_ACC_WORDS(RT_NS::real) * 8 * rt_block_of(variant)) : 0;
 }
 
 int rt_launch_render(const KernelParamsT<RT_NS::real>& p, int grid_blocks, int variant, void* stream) {
@@ -325,7 +320,7 @@ int rt_launch_render(const KernelParamsT<RT_NS::real>& p, int grid_blocks, int v
   const int block = rt_block_of(variant);
   long long need = ((long long)p.n_items + block - 1) / block;
   int grid = need < grid_blocks ? (int)need : grid_blocks;
-  size_t lds = render_lds_bytes(p.stack_depth, variant, p.lds_nodes, p.n_media);
+  size_t lds = render_lds_bytes(p.stack_depth, variant, p.lds_nodes);
   hipLaunchKernelGGL(render_kernel_of(variant), dim3(grid), dim3(block), lds, (hipStream_t)stream, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

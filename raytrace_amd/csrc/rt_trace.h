@@ -1673,16 +1673,9 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
 // entering it, the second (Geometry.hs:306-328) — each starting inside the traversal loop as
 // soon as the previous one finishes.
 enum : int { ST_NEED_ITEM = 0, ST_NEED_SAMPLE = 1, ST_START_SEG = 2, ST_TRACE = 3, ST_SHADE = 4 };
-// Media events of a segment (constantMedium's free-flight draw over a boundary interval,
-// Geometry.hs:312-328) are not drawn where the traversal chain finds their interval — inside the
-// traversal rounds, with the few lanes whose query just finished — but recorded (lo, hi per
-// medium, in LDS: `pend`, word-major, `pstride` apart) and drawn when the segment shades, in
-// medium order, all lanes together.  Same draws (counter-based, keyed by the medium), same order of
-// the tbest updates, so the same hit; the chain's entering test (t1 < tbest) then sees the surface
-// hit without earlier media draws, which can only start an exit query whose draw cannot win.
 template <int kTex, bool kMedia, bool kMats, bool kInst, class Grab, class Commit, class AccT>
 RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW, const real* prims_,
-                        AccT& acc, real* pend = nullptr, int pstride = 0) {
+                        AccT& acc) {
   const cfp prims = cf(prims_);
   const int n_media = kMedia ? P.n_media : 0;  // media code only in the kMedia instantiations
   int overflow = 0;
@@ -1709,12 +1702,6 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
   trav_begin(S, RT_EMPTY_ROOT, kTmin);
   // query sequencing within a segment: q = 0 surfaces; q = 1 + 2m / 2 + 2m medium m, 1st / 2nd hit
   int q = 0, best = -1, hit_medium = -1, best_inst = -1;
-  unsigned pending = 0u;  // media whose event waits for the shading phase (bit m)
-  auto defer_event = [&](int m, real lo, real hi) {
-    pend[(2 * m) * pstride] = lo;
-    pend[(2 * m + 1) * pstride] = hi;
-    pending |= 1u << m;
-  };
   real tbest = kInf, t1 = RL(0.0), t_surf = kInf;
   RT_PROF_DECL
   for (;;) {
@@ -1781,17 +1768,17 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
                     next_m = -1;
                   }
                 } else {
-                  defer_event(m, kTmin, t1);
+                  medium_event(P, m, I.pix, I.sample, seg, kTmin, t1, tbest, hit_medium);
                 }
               }
             } else if (S.C.prim >= 0) {  // exit hit of medium m
-              defer_event(m, t1, S.C.t);
+              medium_event(P, m, I.pix, I.sample, seg, t1, S.C.t, tbest, hit_medium);
             }
           }
           // media whose boundary is the surface set reuse the surface hit (DevMedium)
           while (next_m >= 0 && next_m < n_media && P.media[next_m].alias_surface) {
             if (best >= 0 && !prim_front(P, prims, best, R, t_surf))
-              defer_event(next_m, kTmin, t_surf);
+              medium_event(P, next_m, I.pix, I.sample, seg, kTmin, t_surf, tbest, hit_medium);
             ++next_m;
           }
           if (next_m >= 0) {
@@ -1812,13 +1799,6 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
     RT_PROF_ADD(PF_SHADING, RT_BALLOT_COUNT(state == ST_SHADE));
     // ---- shade the segments whose queries are complete
     if (state == ST_SHADE) {
-      if constexpr (kMedia) {
-        for (int m = 0; m < n_media; ++m)
-          if (pending & (1u << m))
-            medium_event(P, m, I.pix, I.sample, seg, pend[(2 * m) * pstride], pend[(2 * m + 1) * pstride], tbest,
-                         hit_medium);
-        pending = 0u;
-      }
       f3 L = mk3(RL(0.), RL(0.), RL(0.));
       if (shade<kTex, kMats, kInst>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T, best_inst)) {
         RT_HOOK_SAMPLE(I.pix, I.sample, L);

@@ -34,14 +34,12 @@ int run_loop(const RT_NS::KernelParams& P, int variant, G& g, Cm& c, const RT_NS
   // the item sums through the device kernels' LDS accumulator (one lane: stride 1)
   unsigned long long words[6] = {0, 0, 0, 0, 0, 0};
   RT_NS::AccLds acc{words, 1};
-  RT_NS::real pend[2 * RT_MAX_MEDIA];  // deferred media events (one lane: stride 1)
-  if (variant & RT_VAR_INST)
-    return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, true>(P, g, c, W, P.prims, acc, pend, 1);
+  if (variant & RT_VAR_INST) return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, true>(P, g, c, W, P.prims, acc);
   switch (variant & RT_VAR_BASE) {
     case RT_VAR_FLAT: return RT_NS::lane_loop_lockstep<true, kTex, kMedia, kMats>(P, g, c, W, P.prims, acc);
     case RT_VAR_BVH_LOCKSTEP:
       return RT_NS::lane_loop_lockstep<false, kTex, kMedia, kMats>(P, g, c, W, P.prims, acc);
-    default: return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, false>(P, g, c, W, P.prims, acc, pend, 1);
+    default: return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, false>(P, g, c, W, P.prims, acc);
   }
 }
 template <int kTex, class G, class Cm>
