@@ -12,8 +12,10 @@ tensor) inside the timed region — asynchronously, so frame i+1 renders while f
 flight (two frame buffers); the clock stops after every frame is rendered AND gathered.
 `value` = pixels x spp of all ranks / max-over-ranks time.
 The W warm-up frames are followed by more untimed frames until the warm-up has rendered for
---warmup-s seconds (0.5 by default; the per-frame time only settles after a few hundred ms of
-continuous rendering); `warmup_frames` / `warmup_s` in the line say how many ran.
+--warmup-s seconds (2 by default: the per-frame time only settles after a few hundred ms of
+continuous rendering, and a GPU-activity sampler polling about once a second sees the card busy
+even when the timed region itself is a fraction of a second); `warmup_frames` / `warmup_s` in the
+line say how many ran.
 
 Frames of flat scenes (the Cornell box) alternate between two HIP streams (--streams 2, the
 default for them): a frame's last long paths occupy few CUs, and the next frame's persistent
@@ -230,7 +232,7 @@ def main():
                     help="frames alternate between this many HIP streams (2: frame i+1 fills the CUs that "
                          "frame i's last long paths leave idle); 0 = auto: 2 for flat scenes, 1 for BVH "
                          "scenes (two LDS-staging BVH launches interfere: bunny 20.7 -> 22.4 ms per frame)")
-    ap.add_argument("--warmup-s", type=float, default=0.5,
+    ap.add_argument("--warmup-s", type=float, default=2.0,
                     help="after the W warm-up frames, keep warming up until the warm-up has rendered this "
                          "many seconds (the per-frame time settles after a few hundred ms); 0: exactly W")
     ap.add_argument("--sim-shards", type=int, default=1,
