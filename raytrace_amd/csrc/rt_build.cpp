@@ -877,6 +877,10 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
     return fail(err, RT_E_INVALID, "non-finite camera settings");
   int rows = rt_host_shard_rows(h, ex);
   if (rows < 0) return fail(err, RT_E_INVALID, "invalid rt_exec");
+  // pixel and work-item ids are 32-bit ints: one render's tile holds at most 0x7fffff00 pixels
+  if ((long long)rows * cs->image_width > 0x7fffff00LL)
+    return fail(err, RT_E_UNSUPPORTED, "a tile of %d x %d pixels exceeds 2^31 (split it over shards)", cs->image_width,
+                rows);
   // Ray.hs:122-136, 153-155 in binary64, rounded once to R
   d3 center = D3(cs->center), look = D3(cs->look_at), up = D3(cs->up);
   double vh = cs->focus_dist * std::tan(cs->vfov / 2) * 2;

@@ -221,24 +221,28 @@ void rt_render_kernel(KernelParams P) {
   if (overflow) atomicOr(P.status, 1);
 }
 
-// mean over spp (Ray.hs:232) from the fixed-point sums; NaN where a sample was non-finite
+// mean over spp (Ray.hs:232) from the fixed-point sums; NaN where a sample was non-finite.  One
+// thread per output word (blockIdx.y = the channel) and the FP32 scale from the host: the kernel
+// needs at most 8 VGPRs, so with two streams it fits beside the next frame's 7-wave FP32 render
+// grid (69 VGPRs, 8 left per SIMD lane) instead of waiting for that grid to drain
 __global__ __launch_bounds__(256) void rt_resolve_kernel(const long long* __restrict__ accum,
                                                          const unsigned int* __restrict__ nanflag,
-                                                         real* __restrict__ out, int n_pixels, int spp) {
-  int i = blockIdx.x * 256 + threadIdx.x;
+                                                         real* __restrict__ out, int n_pixels, int spp, double scale) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n_pixels) return;
+  const size_t w = 3 * (size_t)i + blockIdx.y;
   const bool bad = nanflag[i] != 0u;
-  const long long* a = accum + RT_ACC_WORDS(real) * (size_t)i;
-  for (int c = 0; c < 3; ++c) {
 #if RT_F64
-    // (hi + lo 2^-32) 2^-32 / spp: the integer words are exact in binary64 (< 2^53), one rounding
-    // for the sum, one for the mean
-    const double sum = ((double)a[c] + (double)(unsigned long long)a[3 + c] * (1.0 / RT_FIX_SCALE)) * (1.0 / RT_FIX_SCALE);
-    out[3 * (size_t)i + c] = bad ? __builtin_nan("") : sum / (double)spp;
+  // (hi + lo 2^-32) 2^-32 / spp: the integer words are exact in binary64 (< 2^53), one rounding
+  // for the sum, one for the mean
+  (void)scale;
+  const long long* a = accum + 6 * (size_t)i + blockIdx.y;
+  const double sum = ((double)a[0] + (double)(unsigned long long)a[3] * (1.0 / RT_FIX_SCALE)) * (1.0 / RT_FIX_SCALE);
+  out[w] = bad ? __builtin_nan("") : sum / (double)spp;
 #else
-    out[3 * (size_t)i + c] = bad ? __builtin_nanf("") : (float)((double)a[c] * (1.0 / (RT_FIX_SCALE * (double)spp)));
+  (void)spp;
+  out[w] = bad ? __builtin_nanf("") : (float)((double)accum[w] * scale);  // scale = 2^-32 / spp
 #endif
-  }
 }
 
 static bool acc_in_lds(int variant) {
@@ -308,6 +312,7 @@ int rt_render_waves(const KernelParamsT<RT_NS::real>*, int variant) {
   const bool flat = (variant & RT_VAR_BASE) == RT_VAR_FLAT;
   const int tex = (variant & RT_VAR_NOISE) ? 2 : (variant & RT_VAR_TEX) ? 1 : 0;
   const bool media = (variant & RT_VAR_MEDIA) != 0, mats = (variant & RT_VAR_MATS) != 0;
+  (void)mats;  // the FP32 occupancy table does not depend on the material set
   return RT_WAVES_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats);
 }
 int rt_render_acc_lds(const KernelParamsT<RT_NS::real>*, int variant) {
@@ -341,7 +346,7 @@ int rt_launch_resolve(const KernelParamsT<RT_NS::real>& p, void* stream) {
   using namespace RT_NS;
   int n = p.tile_rows * p.cam.width;
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(rt_resolve_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                     (const long long*)p.accum, p.nanflag, p.out, n, p.cam.spp);
+  hipLaunchKernelGGL(rt_resolve_kernel, dim3((n + 255) / 256, 3), dim3(256), 0, (hipStream_t)stream,
+                     (const long long*)p.accum, p.nanflag, p.out, n, p.cam.spp, 1.0 / (RT_FIX_SCALE * (double)p.cam.spp));
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -128,6 +128,16 @@ def test_scene_validation_errors_before_device():
         R.raytrace(cs.replace(cs_redirectTargets=[(0.01, (0, 0, 0), (1, 0, 0), (0, 1, 0))] * 9), world, seed)
     with pytest.raises(ValueError):
         R.raytrace(cs, world, seed, precision="f16")
+    with pytest.raises(R.RtUnsupported):  # column / row are 16-bit in the kernels
+        R.raytrace(cs.replace(cs_imageWidth=65536, cs_aspectRatio=65536.0), world, seed)
+    # a tile beyond 2^31 pixels (32-bit pixel ids) is refused before any buffer is written
+    L = _lib.load()
+    from raytrace_amd.scene import flatten
+    big = cs.replace(cs_imageWidth=65535, cs_aspectRatio=65535 / 40000)
+    c, sc, ex = _lib.camera_struct(big), _lib.scene_struct(flatten(world)), _lib.exec_struct()
+    out = np.zeros(3)
+    assert L.rt_render(ctypes.byref(c), ctypes.byref(sc), 1, ctypes.byref(ex), out.ctypes.data, None) == _lib.RT_E_UNSUPPORTED
+    assert b"2^31" in L.rt_last_error()
 
 
 def test_device_list_validation_before_device():

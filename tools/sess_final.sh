@@ -15,4 +15,4 @@ import json; d=json.loads(open('$O/bench_$c.json').read().strip().splitlines()[-
 print('$c', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], 'f32', f.get('value'), f.get('ms_per_step'))"; done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_bench.json 2> $O/prof.err || { echo "rocprof failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof1 -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --streams 1 > $O/prof1_bench.json 2> $O/prof1.err || { echo "rocprof 1-stream failed"; exit 1; }
-grep -h "render_kernel\|resolve" $O/prof1/*kernel_stats.csv | cut -c1-200
+for d in prof prof1; do echo $d; grep -h "render_kernel\|resolve" $O/$d/*kernel_stats.csv | cut -c1-160; done
