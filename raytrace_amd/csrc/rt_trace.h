@@ -352,6 +352,12 @@ RT_FN v4f ldc4f(cfpf p) {
 struct u4 {
   uint32_t x, y, z, w;
 };
+// a ^ b ^ c in one VALU instruction: gfx950's three-input bit operation (truth table 0x96)
+#if defined(RT_HOST_EMU) || defined(RT_EXP_XOR2)
+#define RT_XOR3(a, b, c) ((a) ^ (b) ^ (c))
+#else
+#define RT_XOR3(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x96)
+#endif
 RT_FN u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
 #ifndef RT_PHILOX_ROUNDS
 #define RT_PHILOX_ROUNDS 10
@@ -371,7 +377,7 @@ RT_FN u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    uint32_t n0 = RT_XOR3(hi1, c1, k0), n2 = RT_XOR3(hi0, c3, k1);
     c0 = n0;
     c1 = lo1;
     c2 = n2;
