@@ -272,8 +272,10 @@ namespace RT_NS {
 
 #if RT_F64
 using real = double;
+using ureal = unsigned long long;  // the bit pattern of a real
 #else
 using real = float;
+using ureal = uint32_t;
 #endif
 using KernelParams = ::KernelParamsT<real>;
 using DevMaterial = ::DevMaterialT<real>;
@@ -619,7 +621,10 @@ RT_FN void isect_plane(const PrimRec& r, f3 o, const RayCtx& R, real tmin_up, bo
 template <bool kKeyOnly, bool kInst = false>
 RT_FN void consider(Closest& C, real t, real q, int ord, int pi, int inst = -1) {
 #if RT_F64
-  const bool take = q >= RL(0.0) && (t < C.t || (t == C.t && ord < C.ord));
+  // flat sets: bitwise, not short-circuit — three compares and mask ANDs instead of nested exec
+  // branches (Cornell -1.4 %); BVH leaves keep the branches (their kernels' SGPR spills grew)
+  const bool take = kKeyOnly ? (q >= RL(0.0)) & ((t < C.t) | ((t == C.t) & (ord < C.ord)))
+                             : q >= RL(0.0) && (t < C.t || (t == C.t && ord < C.ord));
   C.t = take ? t : C.t;
   C.ord = take ? ord : C.ord;
   if constexpr (!kKeyOnly) C.prim = take ? pi : C.prim;
@@ -729,7 +734,13 @@ RT_FN void test_box(const RT_CAS DevBox* B, const RayCtx& R, real tmin_up, Close
 #endif
     const real s = dot(ax[k], oc);
     const real t0 = -s * inv, t1 = RFMA(-s, inv, inv);  // the s = 0 and s = 1 planes
-    flip[k] = t1 < t0 ? 1 : 0;                            // entering through the s = 1 end
+#ifndef RT_EXP_FLIP_CMP
+    // entering through the s = 1 end: t1 - t0 = inv, so t1 < t0 iff inv < 0 (the sign bit; the
+    // two differ only when rounding makes t1 == t0, a slab |s| >= 2^52 box widths away)
+    flip[k] = (int)(__builtin_bit_cast(ureal, inv) >> (8 * sizeof(real) - 1));
+#else
+    flip[k] = t1 < t0 ? 1 : 0;
+#endif
     lo[k] = RMIN(t0, t1);
     hi[k] = RMAX(t0, t1);
   }
