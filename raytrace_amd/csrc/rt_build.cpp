@@ -953,7 +953,6 @@ FastDiv rt_host_fastdiv(uint32_t d) {
 
 template <class R>
 void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_sizes) {
-  P.div_tile = rt_host_fastdiv((uint32_t)P.tile_rows * (uint32_t)P.cam.width);
   P.div_width = rt_host_fastdiv((uint32_t)P.cam.width);
   P.div_block = rt_host_fastdiv((uint32_t)P.row_block);
   P.trav_exit_pct = 50;  // the caller sets the scene's policy (HostScene::trav_exit_pct) afterwards
@@ -1007,8 +1006,19 @@ void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_s
   P.n_chunks = (spp - n_big * big + chunk - 1) / chunk;
   P.big_chunk = big;
   P.n_big_chunks = n_big;
-  P.small_base = n_big * (big - chunk);
+  P.big_items = (int)((long long)n_big * tile_pixels);
+  P.small_start = n_big * big;
+  P.div_big = rt_host_fastdiv((uint32_t)std::max(1, n_big));
+  P.div_small = rt_host_fastdiv((uint32_t)std::max(1, P.n_chunks));
   P.n_items = (int)items;
+  // commit aggregation: a phase qualifies when a pool of RT_POOL consecutive ids spans at most a
+  // slot's pixels (rt_render_kernel.h WaveWork); env RT_AMD_AGG=0 turns it off (A/B, same LDS)
+  const int slot_pix = two_sizes ? RT_AGG_PIX_FLAT : RT_AGG_PIX_BVH;
+  auto spans = [&](int n) { return n > 0 && (RT_POOL - 1 + n - 1) / n + 1 <= slot_pix; };
+  bool agg = tile_pixels < (1ll << 24);  // the item's aggregation code shares its tile-pixel word
+  if (const char* env = std::getenv("RT_AMD_AGG")) agg = agg && std::atoi(env) != 0;
+  P.agg_big = agg && spans(n_big);
+  P.agg_small = agg && spans(P.n_chunks);
 }
 
 template int rt_host_make_params<float>(const rt_camera_settings*, uint64_t, const rt_exec*, KernelParamsT<float>&,

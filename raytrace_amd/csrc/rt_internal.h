@@ -37,6 +37,26 @@
 // small items per resident lane kept for the queue tail (rt_build.cpp rt_host_plan_work; 0: one
 // item size).  Cornell 600x600x200, same box (profiles/r2/items/): binary64 6.77 -> 6.63 ms at
 // 16 (8: 6.69, 32: 6.64, 64: 6.78); FP32 3.50 -> 3.46 at 32 (16: 3.49); 8-GPU shares unchanged
+// Work-item claims: a wave takes RT_POOL consecutive ids per queue atomic (rt_render_kernel.h
+// WaveWork).  64 -> 128: Cornell 4.13 -> 4.04 ms (at 32 the head word saturates: 7.2 ms)
+#ifndef RT_POOL
+#define RT_POOL 128
+#endif
+// Commit aggregation (rt_render_kernel.h WaveWork): per wave, RT_AGG_SLOTS_* LDS slots of
+// RT_AGG_PIX_* pixels' fixed-point words; a pool of RT_POOL ids is aggregated when it lies in one
+// phase whose chunks per pixel n keep its pixel span ceil((RT_POOL - 1) / n) + 1 within a slot
+#ifndef RT_AGG_SLOTS_FLAT
+#define RT_AGG_SLOTS_FLAT 8
+#endif
+#ifndef RT_AGG_PIX_FLAT
+#define RT_AGG_PIX_FLAT 17  // n >= 8
+#endif
+#ifndef RT_AGG_SLOTS_BVH
+#define RT_AGG_SLOTS_BVH 4
+#endif
+#ifndef RT_AGG_PIX_BVH
+#define RT_AGG_PIX_BVH 5  // n >= 32 (the BVH kernels' LDS is node staging too)
+#endif
 #ifndef RT_BIG_CHUNK_MAX
 #define RT_BIG_CHUNK_MAX 16  // samples per big work item at most (rt_build.cpp rt_host_plan_work; 38-48: Cornell f64 +1.5 %)
 #endif
@@ -240,16 +260,23 @@ struct KernelParamsT {
   unsigned long long* accum;  // fixed-point radiance sums per tile pixel: RT_ACC_WORDS(R) x int64
   unsigned int* nanflag;      // per tile pixel: a sample produced a non-finite radiance
   int* counter;               // next unclaimed item
-  // two item sizes: the first n_big_chunks x tile pixels items cover samples
-  // [0, n_big_chunks * big_chunk) of their pixel in big_chunk-sample chunks (fewer commits), the
-  // rest cover the remaining samples in chunk-sample chunks (a short queue tail)
+  // two item sizes: the first big_items = n_big_chunks x tile pixels ids are big items (samples
+  // [0, n_big_chunks * big_chunk) of their pixel in big_chunk-sample chunks: fewer commits), the
+  // rest cover the remaining samples in chunk-sample chunks (a short queue tail).  Within each
+  // phase the ids are PIXEL-major (id = phase start + tile pixel x chunks per pixel + chunk), so
+  // a wave's pool of consecutive ids covers a few pixels (rt_render_kernel.h commit aggregation)
   int chunk;                  // samples per (small) item
   int n_chunks;               // small chunks per pixel
   int n_items;                // all items
   int big_chunk;              // samples per big item
-  int n_big_chunks;           // big chunks per pixel (0: one item size); big items are the first
-                              // n_big_chunks x tile pixels ids
-  int small_base;             // n_big_chunks x (big_chunk - chunk): small chunk k starts at small_base + k chunk
+  int n_big_chunks;           // big chunks per pixel (0: one item size)
+  int big_items;              // n_big_chunks x tile pixels: the first small item's id
+  int small_start;            // n_big_chunks x big_chunk: small chunk k covers [small_start + k chunk, ...)
+  FastDiv div_big, div_small; // by n_big_chunks, by n_chunks (item id -> tile pixel)
+  // commit aggregation (rt_render_kernel.h WaveWork): a phase's items are summed per pixel in the
+  // wave's LDS slots when agg_big / agg_small (its chunks per pixel >= RT_AGG_MIN_N of the kernel
+  // class); 0: every item adds to `accum` directly
+  int agg_big, agg_small;
   int stack_depth;            // LDS stack entries per lane (>= the scene's BVH depth)
   int lds_nodes;              // BVH nodes [0, lds_nodes) are read from the workgroup's LDS copy
   int trav_exit_pct;          // BVH kernel: leave traversal when <= this % of live lanes trace
@@ -266,7 +293,7 @@ struct KernelParamsT {
   DevCameraT<R> cam;
   uint32_t key0, key1;
   int n_shards, shard, row_block, tile_rows;
-  FastDiv div_tile, div_width, div_block;  // tile pixels, image width, row block
+  FastDiv div_width, div_block;  // image width, row block
 };
 using DevMaterial = DevMaterialT<float>;
 using DevTexture = DevTextureT<float>;

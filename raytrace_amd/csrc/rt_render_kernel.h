@@ -29,9 +29,6 @@ namespace {
 // ~88 returning atomics per microsecond, MI355X_MICROARCH.md "dequeue").  Lanes that need work
 // take ids in lane order; ids are never dropped (a pool is contiguous and increasing, so once a
 // lane draws an id >= n_items every later id is out of range too).
-#ifndef RT_POOL
-#define RT_POOL 128  // 64 -> 128: Cornell 4.13 -> 4.04 ms (at 32 the head word saturates: 7.2 ms)
-#endif
 static_assert(RT_POOL >= 64, "a refill must cover every lane of a wave");
 // The dynamic ids [offset, n_items) are split into RT_QUEUES contiguous ranges, each with its own
 // head word (256 B apart): a wave starts on queue (wave % RT_QUEUES) and moves to the next one
@@ -43,15 +40,104 @@ static_assert(RT_POOL >= 64, "a refill must cover every lane of a wave");
 #define RT_QUEUES 4
 #endif
 static_assert((RT_QUEUES & (RT_QUEUES - 1)) == 0 && RT_QUEUES <= 8, "RT_QUEUES: a power of two, at most 8 (workspace)");
-struct WaveGrab {
-  int* counter;  // RT_QUEUES head words, 64 ints apart
+// Per-wave commit aggregation.  Ids are pixel-major (rt_trace.h open_item), so the RT_POOL
+// consecutive ids of one pool cover a few pixels: when a pool is opened the wave gives it one of
+// its kSlots LDS slots (kPix pixels x RT_ACC_WORDS words, pixel-major like `accum`, plus a header:
+// ids still open, first tile pixel; the item carries slot + 1, rt_trace.h ItemCtx).  A finished
+// item adds its words to the slot with LDS atomics instead of 64-bit atomics to HBM and counts
+// its id off; once a pool's ids are all committed the wave adds the slot's words to `accum` —
+// consecutive addresses, one atomic per nonzero word per (pixel, pool) instead of per item — and
+// frees the slot (lazily: when a new pool finds no free slot, and at the end).  A slot belongs to one wave
+// (so no synchronisation beyond the wave's own LDS order); the ids of a pool are claimed by that
+// wave only.  Pools the host did not qualify (a phase with few chunks per pixel, the pool that
+// straddles the two item sizes) or that find every slot busy commit directly, as before.  Integer
+// sums: the image is bit-identical either way.
+static_assert(RT_POOL >= 64, "a refill must cover every lane of a wave");
+#ifndef RT_AGG_CODE_LOCAL
+#define RT_AGG_CODE_LOCAL 0  // 1: (slot << 5 | pixel) + 1, resolved at the item start: no faster (Cornell f64 5.77 vs 5.74 ms, f32 3.41 vs 3.38; profiles/r3/agg)
+#endif
+static_assert(RT_AGG_PIX_FLAT <= 32 && RT_AGG_PIX_BVH <= 32 && (RT_AGG_SLOTS_FLAT - 1) * 32 + RT_AGG_PIX_FLAT <= 255 &&
+                  (RT_AGG_SLOTS_BVH - 1) * 32 + RT_AGG_PIX_BVH <= 255,
+              "(slot << 5 | pixel) + 1 must fit the 8 bits of rt_trace.h ItemCtx::tp");
+// The dynamic ids [offset, n_items) are split into RT_QUEUES contiguous ranges, each with its own
+// head word (256 B apart): a wave starts on queue (wave % RT_QUEUES) and moves to the next one
+// when its queue is spent, so each word sees 1 / RT_QUEUES of the refills.  Measured (kernel ms,
+// 1 / 2 / 4 / 8 queues): README 0.315 / 0.282 / 0.285 / 0.29 (its cheap samples ran the single
+// word near its returning-atomic rate), README on 2 GPUs 0.191 / 0.189 / 0.177 / 0.180, Cornell
+// 3.455 / 3.42 / 3.42 / 3.43, Cornell's 8-GPU share 0.520 / 0.517 / 0.517 / 0.519.
+#ifndef RT_QUEUES
+#define RT_QUEUES 4
+#endif
+static_assert((RT_QUEUES & (RT_QUEUES - 1)) == 0 && RT_QUEUES <= 8, "RT_QUEUES: a power of two, at most 8 (workspace)");
+
+// LDS of the aggregation slots per wave: kSlots x kPix x RT_ACC_WORDS words + 2 kSlots header ints
+template <int kSlots, int kPix>
+struct AggGeom {
+  static constexpr int kWords = kPix * RT_ACC_WORDS(real);  // 64-bit words per slot
+  static constexpr int kWaveBytes = kSlots * kWords * 8 + 2 * kSlots * 4;
+};
+
+template <int kSlots, int kPix>
+struct WaveWork {
+  const KernelParams& P;
+  // item claims: a pool of consecutive ids in SGPRs (wave-uniform state), refilled with ONE
+  // returning atomicAdd of RT_POOL ids, so the head word sees one atomic per RT_POOL claims (a
+  // single word saturates at ~88 returning atomics per microsecond, MI355X_MICROARCH.md
+  // "dequeue").  Lanes that need work take ids in lane order; ids are never dropped (a pool is
+  // contiguous and increasing, so once a lane draws an id >= n_items every later id is too).
   int pool_base;
   int pool_left;
   int offset;  // ids [0, offset) are the waves' initial pools, handed out without atomics
-  int n_items;
-  int queue;  // the queue this wave refills from
-  int spent;  // queues found spent (RT_QUEUES: every id is claimed)
-  __device__ __forceinline__ int operator()(bool need) {
+  int queue;   // the queue this wave refills from
+  int spent;   // queues found spent (RT_QUEUES: every id is claimed)
+  int pool_slot;  // the current pool's slot (-1: direct commits)
+  // aggregation: this wave's slots [kSlots][kWords] and header [open ids x kSlots, tplo x kSlots]
+  unsigned long long* slots;
+  int* hdr;
+  unsigned free_mask;  // wave-uniform
+
+  __device__ __forceinline__ WaveWork(const KernelParams& P_, int wave, int waves, unsigned long long* slots_)
+      : P(P_), pool_base(wave * RT_POOL), pool_left(RT_POOL), offset(waves * RT_POOL), queue(wave & (RT_QUEUES - 1)),
+        spent(0), pool_slot(-1), slots(slots_),
+        hdr(reinterpret_cast<int*>(slots_ + kSlots * AggGeom<kSlots, kPix>::kWords)),
+        free_mask(kSlots > 0 ? (1u << kSlots) - 1u : 0u) {
+    // every wave starts with a static pool (its wave index x RT_POOL): at launch all resident
+    // waves would otherwise queue up on the counter at once (~80 us at ~88 returning atomics per us)
+    pool_slot = open_pool(pool_base, min(RT_POOL, P.n_items - pool_base));
+  }
+
+  // a slot for the pool of ids [b0, b0 + cnt) (wave-uniform), or -1: commit its items directly.
+  // Slots are reclaimed here, lazily: when none is free, every slot whose ids are all committed
+  // is flushed (so the commit path itself never waits on an LDS return or branches to a flush)
+  __device__ __forceinline__ int open_pool(int b0, int cnt) {
+    if (kSlots == 0 || cnt <= 0) return -1;
+    const bool big = b0 < P.big_items;
+    if (big ? (!P.agg_big || b0 + cnt > P.big_items) : !P.agg_small) return -1;
+    if (free_mask == 0u) reclaim();
+    if (free_mask == 0u) return -1;
+    const int tplo = (int)fast_div((uint32_t)(big ? b0 : b0 - P.big_items), big ? P.div_big : P.div_small);
+    const int s = __builtin_ctz(free_mask);
+    free_mask &= free_mask - 1u;
+    hdr[s] = cnt;  // every active lane stores the same words
+    hdr[kSlots + s] = tplo;
+    return s;
+  }
+  __device__ __forceinline__ void reclaim() {
+#pragma unroll 1
+    for (int s = 0; s < kSlots; ++s)
+      if (__builtin_amdgcn_readfirstlane(hdr[s]) == 0) flush(s);
+  }
+  // after the lane loop (every lane of the wave back): flush the slots still held
+  __device__ __forceinline__ void finish() {
+#pragma unroll 1
+    for (int s = 0; s < kSlots; ++s)
+      if (!((free_mask >> s) & 1u)) flush(s);
+  }
+
+  // wave-collective: a fresh item for lanes with need (n_items once every id is claimed), with
+  // its pool's slot
+  __device__ __forceinline__ int grab(bool need, int& slot) {
+    slot = pool_slot;
     const unsigned long long m = __ballot(need);
     if (m == 0ull) return 0;
     const int lane = (int)__lane_id();
@@ -64,6 +150,7 @@ struct WaveGrab {
       return item;
     }
     // ranks [0, pool_left) drain the pool; the others are served by refills, in rank order
+    const int n_items = P.n_items;
     int item = rank < pool_left ? pool_base + rank : n_items;
     int first = pool_left, rest = cnt - pool_left;
     pool_left = 0;
@@ -74,7 +161,7 @@ struct WaveGrab {
       const int qs = offset + queue * len;
       const int qlen = min(len, n_items - qs);  // <= 0 for an empty last queue
       int base = 0;
-      if (lane == leader) base = atomicAdd(counter + 64 * queue, RT_POOL);
+      if (lane == leader) base = atomicAdd(P.counter + 64 * queue, RT_POOL);
       base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
       if (base >= qlen) {  // spent: ids are only ever handed out below qlen
         queue = (queue + 1) & (RT_QUEUES - 1);
@@ -83,7 +170,11 @@ struct WaveGrab {
       }
       const int avail = min(RT_POOL, qlen - base);
       const int take = min(rest, avail);
-      if (rank >= first && rank < first + take) item = qs + base + (rank - first);
+      pool_slot = open_pool(qs + base, avail);
+      if (rank >= first && rank < first + take) {
+        item = qs + base + (rank - first);
+        slot = pool_slot;
+      }
       first += take;
       rest -= take;
       pool_base = qs + base + take;
@@ -93,22 +184,13 @@ struct WaveGrab {
         ++spent;
       }
     }
-    return item;  // n_items for lanes left over once every queue is spent
+    return item;
   }
-};
 
-// A finished item's fixed-point sums (rt_trace.h Acc): RT_ACC_WORDS 64-bit integer atomics per
-// pixel, [hi.xyz] (float) or [hi.xyz, lo.xyz] (binary64); zero words are skipped.
-struct AtomicCommit {
-  unsigned long long* accum;
-  unsigned int* nanflag;
-  template <class AccT>
-  __device__ __forceinline__ void operator()(int tp, const AccT& acc, bool bad) const {
-    const Acc A = acc_words(acc);
-#ifdef RT_EXP_NO_COMMIT  // ablation: drop the sums (wrong image), measures the cost of the atomics
-    if (A.hi[0] != 12345) return;
-#endif
-    unsigned long long* a = accum + RT_ACC_WORDS(real) * (size_t)tp;
+  // wave-collective: lanes with c add their finished item's fixed-point sums (rt_trace.h Acc:
+  // [hi.xyz] or [hi.xyz, lo.xyz]; zero words are skipped) to its pool's slot, or to `accum`
+  __device__ __forceinline__ void direct(int tp, const Acc& A) const {
+    unsigned long long* a = P.accum + RT_ACC_WORDS(real) * (size_t)tp;
 #pragma unroll
     for (int c = 0; c < 3; ++c)
       if (A.hi[c]) atomicAdd(a + c, (unsigned long long)A.hi[c]);
@@ -117,7 +199,69 @@ struct AtomicCommit {
     for (int c = 0; c < 3; ++c)
       if (A.lo[c]) atomicAdd(a + 3 + c, A.lo[c]);
 #endif
-    if (bad) atomicOr(nanflag + tp, 1u);
+  }
+  // an item's tile pixel tagged with its slot code in bits 24-31 (rt_trace.h ItemCtx::tp): 0 for
+  // direct commits, else (slot << 5 | pixel within the slot) + 1 — the slot offset is resolved at
+  // the item's start, so its commit needs no LDS read before the adds
+  __device__ __forceinline__ int tag(int tp, int slot) const {
+    if (slot < 0) return tp;
+#if RT_AGG_CODE_LOCAL
+    return tp | ((((slot << 5) | (tp - hdr[kSlots + slot])) + 1) << 24);
+#else
+    return tp | ((slot + 1) << 24);
+#endif
+  }
+  template <class AccT>
+  __device__ __forceinline__ void commit(bool c, int tpk, const AccT& acc, bool bad) {
+    if (!c) return;
+    const int code = (int)((uint32_t)tpk >> 24);
+    const int tp = code ? tpk & 0xffffff : tpk;
+    const Acc A = acc_words(acc);
+#ifdef RT_EXP_NO_COMMIT  // ablation: drop the sums (wrong image), measures the cost of the atomics
+    if (A.hi[0] == 12345)
+#endif
+    {
+      if (kSlots == 0 || code == 0) {
+        direct(tp, A);
+      } else {
+#if RT_AGG_CODE_LOCAL
+        const int s = (code - 1) >> 5;
+        unsigned long long* w = slots + s * AggGeom<kSlots, kPix>::kWords + ((code - 1) & 31) * RT_ACC_WORDS(real);
+#else
+        const int s = code - 1;
+        unsigned long long* w = slots + s * AggGeom<kSlots, kPix>::kWords + (tp - hdr[kSlots + s]) * RT_ACC_WORDS(real);
+#endif
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          if (A.hi[k]) lds_add(w + k, (unsigned long long)A.hi[k]);
+#if RT_F64
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          if (A.lo[k]) lds_add(w + 3 + k, A.lo[k]);
+#endif
+        __hip_atomic_fetch_add(hdr + s, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // no return
+      }
+    }
+    if (bad) atomicOr(P.nanflag + tp, 1u);
+  }
+  // add a closed slot's words to `accum` (consecutive pixels: consecutive addresses) and free it
+  __device__ __forceinline__ void flush(int s) {
+    constexpr int kW = AggGeom<kSlots, kPix>::kWords;
+    const unsigned long long act = __ballot(true);
+    const int k = (int)__popcll(act);
+    const int r = (int)__popcll(act & ((1ull << __lane_id()) - 1ull));
+    const int tplo = __builtin_amdgcn_readfirstlane(hdr[kSlots + s]);
+    const long long g0 = (long long)tplo * RT_ACC_WORDS(real);
+    const long long g_end = (long long)P.tile_rows * P.cam.width * RT_ACC_WORDS(real);
+    unsigned long long* w = slots + s * kW;
+    for (int j = r; j < kW; j += k) {
+      const unsigned long long v = w[j];
+      if (v != 0ull) {
+        w[j] = 0ull;
+        if (g0 + j < g_end) atomicAdd(P.accum + g0 + j, v);
+      }
+    }
+    free_mask |= 1u << s;
   }
 };
 
@@ -178,21 +322,25 @@ struct AtomicCommit {
   ((kVar) == RT_VAR_FLAT ? ((kTex) == 2 ? RT_WAVES_FLAT_NOISE : (kTex) == 0 ? RT_WAVES_FLAT_TEX0 : RT_WAVES_FLAT) \
                          : ((kTex) == 0 && !(kMedia) ? RT_WAVES_BVH_LITE : RT_WAVES_BVH))
 #endif
+// commit-aggregation slots per wave and pixels per slot of a kernel class (rt_internal.h)
+#define RT_AGG_SLOTS_OF(kVar) ((kVar) == RT_VAR_FLAT ? RT_AGG_SLOTS_FLAT : RT_AGG_SLOTS_BVH)
+#define RT_AGG_PIX_OF(kVar) ((kVar) == RT_VAR_FLAT ? RT_AGG_PIX_FLAT : RT_AGG_PIX_BVH)
 template <int kVar, int kTex, bool kMedia, bool kMats, bool kInst>
 __global__ __launch_bounds__(kVar == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH)
 __attribute__((amdgpu_waves_per_eu(RT_WAVES_OF(kVar, kTex, kMedia, kMats))))
 void rt_render_kernel(KernelParams P) {
   extern __shared__ int smem[];
-  // every wave starts with a static pool (its wave index x RT_POOL): at launch all resident waves
-  // would otherwise queue up on the counter at once (~80 us at ~88 returning atomics per us)
+  constexpr int kSlots = RT_AGG_SLOTS_OF(kVar), kPix = RT_AGG_PIX_OF(kVar);
+  constexpr int kAggBytes = AggGeom<kSlots, kPix>::kWaveBytes;
   const int waves = (int)(gridDim.x * (blockDim.x / 64));
-  const int wave = (int)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
-  WaveGrab grab{P.counter, wave * RT_POOL, RT_POOL, waves * RT_POOL, P.n_items, wave & (RT_QUEUES - 1), 0};
-  AtomicCommit commit{P.accum, P.nanflag};
+  // wave-uniform (readfirstlane: the compiler cannot tell that threadIdx.x / 64 is), so the work
+  // state and the slot pointers below live in SGPRs
+  const int wave_in_block = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
+  const int wave = (int)blockIdx.x * (int)(blockDim.x / 64) + wave_in_block;
   int overflow;
-  // LDS: the lanes' item sums [RT_ACC_WORDS][block] (rt_trace.h AccLds), then (BVH kernels)
-  // [stack_depth + 1][RT_BLOCK_BVH] stack words (the last row a spare write target) and the top
-  // P.lds_nodes BVH nodes (64 B each)
+  // LDS: the lanes' item sums [RT_ACC_WORDS][block] (rt_trace.h AccLds; BVH kernels), the waves'
+  // commit-aggregation slots (kAggBytes each), then (BVH kernels) [stack_depth + 1][RT_BLOCK_BVH]
+  // stack words (the last row a spare write target) and the top P.lds_nodes BVH nodes (64 B each)
   using AccT = typename std::conditional<RT_ACC_LDS_OF(kVar, kMedia), AccLds, Acc>::type;
   AccT acc;
   int* smem_rest = smem;
@@ -200,10 +348,14 @@ void rt_render_kernel(KernelParams P) {
     acc = AccLds{reinterpret_cast<unsigned long long*>(smem) + threadIdx.x, (int)blockDim.x};
     smem_rest = smem + 2 * RT_ACC_WORDS(real) * (int)blockDim.x;
   }
+  // this wave's slots, zeroed by the wave itself (nothing else touches them: no barrier)
+  unsigned long long* agg = reinterpret_cast<unsigned long long*>(smem_rest) + kAggBytes / 8 * wave_in_block;
+  smem_rest += kAggBytes / 4 * (int)(blockDim.x / 64);
+  for (int i = (int)__lane_id(); i < kAggBytes / 8; i += 64) agg[i] = 0ull;
   if constexpr (kVar == RT_VAR_FLAT) {
-    overflow = lane_loop_lockstep<true, kTex, kMedia, kMats>(P, grab, commit, Trav{nullptr, 0, nullptr}, P.prims,
-                                                              acc);
-    (void)smem_rest;
+    WaveWork<kSlots, kPix> work(P, wave, waves, agg);
+    overflow = lane_loop_lockstep<true, kTex, kMedia, kMats>(P, work, Trav{nullptr, 0, nullptr}, P.prims, acc);
+    work.finish();
   } else {
     v4f* lds_nodes = reinterpret_cast<v4f*>(smem_rest + (P.stack_depth + 1) * RT_BLOCK_BVH);
     const float4* src = reinterpret_cast<const float4*>(P.nodes);
@@ -212,11 +364,13 @@ void rt_render_kernel(KernelParams P) {
       lds_nodes[i] = v4f{q.x, q.y, q.z, q.w};
     }
     __syncthreads();
+    WaveWork<kSlots, kPix> work(P, wave, waves, agg);
     const Trav W{smem_rest + threadIdx.x, RT_BLOCK_BVH, lds_nodes};
     if constexpr (kVar == RT_VAR_BVH_LOCKSTEP)
-      overflow = lane_loop_lockstep<false, kTex, kMedia, kMats>(P, grab, commit, W, P.prims, acc);
+      overflow = lane_loop_lockstep<false, kTex, kMedia, kMats>(P, work, W, P.prims, acc);
     else
-      overflow = lane_loop_bvh<kTex, kMedia, kMats, kInst>(P, grab, commit, W, P.prims, acc);
+      overflow = lane_loop_bvh<kTex, kMedia, kMats, kInst>(P, work, W, P.prims, acc);
+    work.finish();
   }
   if (overflow) atomicOr(P.status, 1);
 }
@@ -248,9 +402,17 @@ __global__ __launch_bounds__(256) void rt_resolve_kernel(const long long* __rest
 static bool acc_in_lds(int variant) {
   return RT_ACC_LDS_OF((variant & RT_VAR_BASE) == RT_VAR_FLAT ? RT_VAR_FLAT : RT_VAR_BVH, (variant & RT_VAR_MEDIA) != 0);
 }
-static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
+// LDS besides the stacks and the staged nodes: the lanes' item sums and the aggregation slots
+static size_t render_fixed_lds(int variant) {
+  const bool flat = (variant & RT_VAR_BASE) == RT_VAR_FLAT;
   const size_t acc = acc_in_lds(variant) ? (size_t)RT_ACC_WORDS(real) * 8 * rt_block_of(variant) : 0;
-  return acc + ((variant & RT_VAR_BASE) == RT_VAR_FLAT
+  const size_t agg = (size_t)(flat ? AggGeom<RT_AGG_SLOTS_FLAT, RT_AGG_PIX_FLAT>::kWaveBytes
+                                   : AggGeom<RT_AGG_SLOTS_BVH, RT_AGG_PIX_BVH>::kWaveBytes) *
+                     (rt_block_of(variant) / 64);
+  return acc + agg;
+}
+static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
+  return render_fixed_lds(variant) + ((variant & RT_VAR_BASE) == RT_VAR_FLAT
                     ? 0
                     : (size_t)(stack_depth + 1) * RT_BLOCK_BVH * sizeof(int) + (size_t)lds_nodes * 64);
 }
@@ -316,7 +478,7 @@ int rt_render_waves(const KernelParamsT<RT_NS::real>*, int variant) {
   return RT_WAVES_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats);
 }
 int rt_render_acc_lds(const KernelParamsT<RT_NS::real>*, int variant) {
-  return RT_NS::acc_in_lds(variant) ? (int)(RT_ACC_WORDS(RT_NS::real) * 8 * rt_block_of(variant)) : 0;
+  return (int)RT_NS::render_fixed_lds(variant);
 }
 
 int rt_launch_render(const KernelParamsT<RT_NS::real>& p, int grid_blocks, int variant, void* stream) {

@@ -3,7 +3,7 @@
 // Work decomposition: the frame (this shard's rows) x spp is cut into ITEMS = (tile pixel,
 // chunk of consecutive samples).  Lanes are persistent: a lane whose item is exhausted claims
 // the next item from its wave's pool, refilled from one of four queue head words (one
-// wave-aggregated atomic per 128 items; rt_kernel.hip WaveGrab), so every lane
+// wave-aggregated atomic per 128 items; rt_render_kernel.h WaveWork), so every lane
 // stays busy until the queue drains and the tail is one chunk long.  Inside an item a lane
 // regenerates paths: when a path terminates the next sample starts at once.  Per segment:
 //   1. closest hit: flat sets (class loops and box groups over wave-uniform records), or the
@@ -1558,9 +1558,13 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
   return terminate;
 }
 
-// Work item -> pixel / sample range (items are claimed in pixel order, chunk index slowest).
+// Work item -> pixel / sample range.  Ids are pixel-major within each item size (rt_internal.h
+// KernelParams): a pixel's chunks are consecutive ids, so a wave's pool of consecutive ids
+// covers a few pixels and their sums can be aggregated in LDS before the commit atomics.
 struct ItemCtx {
-  int tp;  // tile pixel (-1: no item yet)
+  // tile pixel (-1: no item yet); an item aggregated in an LDS slot carries its slot code in bits
+  // 24-31 (the host aggregates only tiles below 2^24 pixels; rt_render_kernel.h WaveWork::tag)
+  int tp;
   int sample, s_end;
   uint32_t pix;   // global pixel gy * width + px
   uint32_t pxgy;  // gy << 16 | px (rt_build.cpp limits images to 65535 x 65535)
@@ -1569,35 +1573,36 @@ struct ItemCtx {
 // rt_host_plan_work, so their register allocation does not carry the decode)
 template <bool kTwoSizes>
 RT_FN bool open_item(const KernelParams& P, int item, ItemCtx& I) {
-  const int W = P.cam.width, tile_pixels = P.tile_rows * W;
+  const int W = P.cam.width;
   // item, tile pixel and row are non-negative: exact multiply-shift division by the launch
   // constants instead of the ~20-instruction signed integer division sequences
-  const int k = (int)fast_div((uint32_t)item, P.div_tile);
-  I.tp = item - k * tile_pixels;
+  const bool big = kTwoSizes && item < P.big_items;
+  const int id = kTwoSizes && !big ? item - P.big_items : item;
+  const int n = big ? P.n_big_chunks : P.n_chunks;
+  I.tp = (int)fast_div((uint32_t)id, big ? P.div_big : P.div_small);
+  const int k = id - I.tp * n;
   const int tr = (int)fast_div((uint32_t)I.tp, P.div_width);
   const int px = I.tp - tr * W;
   const int tb = (int)fast_div((uint32_t)tr, P.div_block);
   const int gy = (tb * P.n_shards + P.shard) * P.row_block + (tr - tb * P.row_block);
   I.pix = (uint32_t)(gy * W + px);
   I.pxgy = (uint32_t)gy << 16 | (uint32_t)px;
-  // chunks k < n_big_chunks are big (samples [k big_chunk, (k + 1) big_chunk)), the rest small
-  // (from n_big_chunks big_chunk = small_base + n_big_chunks chunk on)
-  const bool big = kTwoSizes && k < P.n_big_chunks;
+  // big chunk k: samples [k big_chunk, (k + 1) big_chunk); small chunk k: from small_start + k chunk
   const int chunk = big ? P.big_chunk : P.chunk;
-  I.sample = (big ? 0 : kTwoSizes ? P.small_base : 0) + k * chunk;
+  I.sample = (big || !kTwoSizes ? 0 : P.small_start) + k * chunk;
   I.s_end = I.sample + chunk < P.cam.spp ? I.sample + chunk : P.cam.spp;
   if (gy >= P.cam.height || P.cam.max_depth <= 0) I.s_end = I.sample;  // padding row / black image
   return I.sample < I.s_end;
 }
 
-// The lockstep persistent lane loop.  `grab(need)` is wave-collective: it returns a fresh item
-// for lanes with need == true.  `commit(tile_pixel, acc, bad)` adds a finished item's
-// sums.  One segment per iteration, all of its queries run by the whole wave together: the flat
+// The lockstep persistent lane loop.  `work.grab(need, slot)` is wave-collective: it
+// returns a fresh item for lanes with need == true (and its aggregation slot); `work.commit(c,
+// tile_pixel, acc, bad)`, also wave-collective, adds the finished items' sums of lanes with
+// c == true.  One segment per iteration, all of its queries run by the whole wave together: the flat
 // kernel (every lane tests the same primitives), and the lockstep BVH variant kept for
 // experiments (RT_VAR_BVH_LOCKSTEP; BVH scenes, media or not, default to lane_loop_bvh).
-template <bool kFlat, int kTex, bool kMedia, bool kMats, class Grab, class Commit, class AccT>
-RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW,
-                             const real* prims_, AccT& acc) {
+template <bool kFlat, int kTex, bool kMedia, bool kMats, class Work, class AccT>
+RT_FN int lane_loop_lockstep(const KernelParams& P, Work& work, const Trav& TW, const real* prims_, AccT& acc) {
   const cfp prims = cf(prims_);
   int overflow = 0;
   ItemCtx I{-1, 0, 0, 0u, 0u};
@@ -1618,13 +1623,16 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
   R.self_inst = -1;
   for (;;) {
     const bool need = !alive && I.sample >= I.s_end;
-    if (need && I.tp >= 0) commit(I.tp, acc, bad);
-    const int got = grab(need);
+    work.commit(need && I.tp != -1, I.tp, acc, bad);
+    int aslot;
+    const int got = work.grab(need, aslot);
     if (need) {
       if (got >= P.n_items) break;
       acc_clear(acc);
       bad = false;
-      if (!open_item<kFlat>(P, got, I)) continue;
+      const bool ok = open_item<kFlat>(P, got, I);
+      I.tp = work.tag(I.tp, aslot);
+      if (!ok) continue;
     }
     if (!alive) {
       camera_ray(P, I.pix, I.sample, I.pxgy, R);
@@ -1690,9 +1698,8 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Grab& grab, Commit& commit, 
 // entering it, the second (Geometry.hs:306-328) — each starting inside the traversal loop as
 // soon as the previous one finishes.
 enum : int { ST_NEED_ITEM = 0, ST_NEED_SAMPLE = 1, ST_START_SEG = 2, ST_TRACE = 3, ST_SHADE = 4 };
-template <int kTex, bool kMedia, bool kMats, bool kInst, class Grab, class Commit, class AccT>
-RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const Trav& TW, const real* prims_,
-                        AccT& acc) {
+template <int kTex, bool kMedia, bool kMats, bool kInst, class Work, class AccT>
+RT_FN int lane_loop_bvh(const KernelParams& P, Work& work, const Trav& TW, const real* prims_, AccT& acc) {
   const cfp prims = cf(prims_);
   const int n_media = kMedia ? P.n_media : 0;  // media code only in the kMedia instantiations
   int overflow = 0;
@@ -1726,13 +1733,15 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Grab& grab, Commit& commit, const
     const bool need = state == ST_NEED_ITEM;
     RT_PROF_ADD(PF_ITERS, 1);
     RT_PROF_ADD(PF_FRONT_LANES, RT_BALLOT_COUNT(state != ST_TRACE));
-    if (need && I.tp >= 0) commit(I.tp, acc, bad);
-    const int got = grab(need);
+    work.commit(need && I.tp != -1, I.tp, acc, bad);
+    int aslot;
+    const int got = work.grab(need, aslot);
     if (need) {
       if (got >= P.n_items) break;
       acc_clear(acc);
       bad = false;
       state = open_item<false>(P, got, I) ? ST_NEED_SAMPLE : ST_NEED_ITEM;
+      I.tp = work.tag(I.tp, aslot);
     }
     if (state == ST_NEED_SAMPLE) {
       camera_ray(P, I.pix, I.sample, ~0u, R);

@@ -11,59 +11,64 @@ struct Shared {
   std::atomic<long long> cnt[4];
 };
 
-struct Grab {
+// the device kernel's WaveWork without waves: one shared counter, every item committed directly
+struct Work {
   Shared* s;
-  int operator()(bool need) { return need ? s->next.fetch_add(1) : 0; }
-};
-struct Commit {
-  Shared* s;
+  int grab(bool need, int& slot) {
+    slot = -1;
+    return need ? s->next.fetch_add(1) : 0;
+  }
+  int tag(int tp, int slot) const {
+    (void)slot;
+    return tp;
+  }
   template <class AccT>
-  void operator()(int tp, const AccT& acc, bool bad) {
+  void commit(bool c, int tp, const AccT& acc, bool bad) {
+    if (!c) return;
     const RT_NS::Acc A = RT_NS::acc_words(acc);
     const size_t w = RT_ACC_WORDS(RT_NS::real);
-    for (int c = 0; c < 3; ++c) (*s->accum)[w * (size_t)tp + c] += A.hi[c];
+    for (int k = 0; k < 3; ++k) (*s->accum)[w * (size_t)tp + k] += A.hi[k];
 #if RT_F64
-    for (int c = 0; c < 3; ++c) (*s->accum)[w * (size_t)tp + 3 + c] += (long long)A.lo[c];
+    for (int k = 0; k < 3; ++k) (*s->accum)[w * (size_t)tp + 3 + k] += (long long)A.lo[k];
 #endif
     if (bad) (*s->flags)[tp] |= 1u;
   }
 };
 
-template <int kTex, bool kMedia, bool kMats, class G, class Cm>
-int run_loop(const RT_NS::KernelParams& P, int variant, G& g, Cm& c, const RT_NS::Trav& W) {
+template <int kTex, bool kMedia, bool kMats, class G>
+int run_loop(const RT_NS::KernelParams& P, int variant, G& g, const RT_NS::Trav& W) {
   // the item sums through the device kernels' LDS accumulator (one lane: stride 1)
   unsigned long long words[6] = {0, 0, 0, 0, 0, 0};
   RT_NS::AccLds acc{words, 1};
-  if (variant & RT_VAR_INST) return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, true>(P, g, c, W, P.prims, acc);
+  if (variant & RT_VAR_INST) return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, true>(P, g, W, P.prims, acc);
   switch (variant & RT_VAR_BASE) {
-    case RT_VAR_FLAT: return RT_NS::lane_loop_lockstep<true, kTex, kMedia, kMats>(P, g, c, W, P.prims, acc);
+    case RT_VAR_FLAT: return RT_NS::lane_loop_lockstep<true, kTex, kMedia, kMats>(P, g, W, P.prims, acc);
     case RT_VAR_BVH_LOCKSTEP:
-      return RT_NS::lane_loop_lockstep<false, kTex, kMedia, kMats>(P, g, c, W, P.prims, acc);
-    default: return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, false>(P, g, c, W, P.prims, acc);
+      return RT_NS::lane_loop_lockstep<false, kTex, kMedia, kMats>(P, g, W, P.prims, acc);
+    default: return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, false>(P, g, W, P.prims, acc);
   }
 }
-template <int kTex, class G, class Cm>
-int run_flags(const RT_NS::KernelParams& P, int variant, G& g, Cm& c, const RT_NS::Trav& W) {
+template <int kTex, class G>
+int run_flags(const RT_NS::KernelParams& P, int variant, G& g, const RT_NS::Trav& W) {
   const int base = variant;
   const bool media = (variant & RT_VAR_MEDIA) != 0, mats = (variant & RT_VAR_MATS) != 0;
-  if (media) return mats ? run_loop<kTex, true, true>(P, base, g, c, W) : run_loop<kTex, true, false>(P, base, g, c, W);
-  return mats ? run_loop<kTex, false, true>(P, base, g, c, W) : run_loop<kTex, false, false>(P, base, g, c, W);
+  if (media) return mats ? run_loop<kTex, true, true>(P, base, g, W) : run_loop<kTex, true, false>(P, base, g, W);
+  return mats ? run_loop<kTex, false, true>(P, base, g, W) : run_loop<kTex, false, false>(P, base, g, W);
 }
-template <class G, class Cm>
-int run_variant(const RT_NS::KernelParams& P, int variant, G& g, Cm& c, const RT_NS::Trav& W) {
-  if (variant & RT_VAR_NOISE) return run_flags<2>(P, variant, g, c, W);
-  if (variant & RT_VAR_TEX) return run_flags<1>(P, variant, g, c, W);
-  return run_flags<0>(P, variant, g, c, W);
+template <class G>
+int run_variant(const RT_NS::KernelParams& P, int variant, G& g, const RT_NS::Trav& W) {
+  if (variant & RT_VAR_NOISE) return run_flags<2>(P, variant, g, W);
+  if (variant & RT_VAR_TEX) return run_flags<1>(P, variant, g, W);
+  return run_flags<0>(P, variant, g, W);
 }
 
 void* worker(void* arg) {
   Shared* s = (Shared*)arg;
   std::vector<int> stack(s->P->stack_depth + 1);
   for (auto& c : rt_emu::counters) c = 0;
-  Grab g{s};
-  Commit c{s};
+  Work g{s};
   const RT_NS::Trav W{stack.data(), 1, nullptr};  // the emulator reads every node from memory
-  int ov = run_variant(*s->P, s->variant, g, c, W);
+  int ov = run_variant(*s->P, s->variant, g, W);
   if (ov) s->overflow = 1;
   for (int i = 0; i < 4; ++i) s->cnt[i] += rt_emu::counters[i];
   return nullptr;
@@ -107,7 +112,9 @@ int render(const HostScene& H, const rt_camera_settings* cs, uint64_t seed, cons
     P.chunk = chunk;
     P.n_chunks = (P.cam.spp + chunk - 1) / chunk;
     P.n_big_chunks = 0;
-    P.small_base = 0;
+    P.big_items = 0;
+    P.small_start = 0;
+    P.div_small = rt_host_fastdiv((uint32_t)P.n_chunks);
     P.n_items = P.n_chunks * P.tile_rows * P.cam.width;
   }
   const size_t tile_pixels = (size_t)P.tile_rows * P.cam.width;

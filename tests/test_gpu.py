@@ -247,6 +247,28 @@ def test_item_chunk_does_not_change_the_image(gpu, monkeypatch, name, precision)
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("name", ["cornell", "bunny_cornell", "pawn_fog"])
+def test_commit_aggregation_is_exact(gpu, monkeypatch, name, precision):
+    """Items summed per pixel in the waves' LDS slots before the commit atomics (rt_render_kernel.h
+    WaveWork) against every item committed directly (RT_AMD_AGG=0): bit-identical images, with one
+    item size (32 / 128 chunks per pixel: flat and BVH kernels aggregate) and with two sizes (a
+    pool straddling the size boundary, big items of 8 samples: 8 per pixel)."""
+    fn = {"cornell": scenes.cornell_box, "bunny_cornell": scenes.bunny_cornell, "pawn_fog": scenes.pawn_fog}[name]
+    cs, world, seed = fn(width=96, spp=128)
+    for env in ({}, {"RT_AMD_CHUNK": "1"}, {"RT_AMD_BIG_CHUNK": "8", "RT_AMD_TAIL_SAMPLES": "64"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        monkeypatch.delenv("RT_AMD_AGG", raising=False)
+        a = R.raytrace(cs, world, seed, precision=precision)
+        monkeypatch.setenv("RT_AMD_AGG", "0")
+        b = R.raytrace(cs, world, seed, precision=precision)
+        assert np.isfinite(a).all() and a.mean() > 0
+        assert np.array_equal(a, b, equal_nan=True), (name, env)
+        for k in env:
+            monkeypatch.delenv(k)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
 def test_medium_boundary_alias_is_exact(gpu, monkeypatch, precision):
     cs, world, seed = scenes.pawn_fog(width=96, spp=8)
     a = R.raytrace(cs, world, seed, precision=precision)

@@ -12,8 +12,14 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # (scene, kwargs): full resolution, reduced samples per pixel
+# (the 128-spp cases split each pixel into 32+ items: the kernels' commit aggregation is active)
 CASES = [("cornell_box", {"spp": 8}), ("bunny_cornell", {"spp": 4}), ("demo1", {"spp": 4}),
-         ("pawn_fog", {"spp": 2}), ("bunny_instances", {}), ("box_gallery", {})]
+         ("pawn_fog", {"spp": 2}), ("bunny_instances", {}), ("box_gallery", {}),
+         ("cornell_box", {"spp": 128}), ("bunny_cornell", {"spp": 128}), ("pawn_fog", {"spp": 128})]
+
+
+def _tag(name, kw):
+    return name + "".join(f"_{k}{v}" for k, v in sorted(kw.items()))
 
 
 def child(out_dir):
@@ -23,7 +29,8 @@ def child(out_dir):
     for name, kw in CASES:
         cs, world, seed = getattr(scenes, name)(**kw)
         for prec in ("f64", "f32"):
-            np.save(os.path.join(out_dir, f"{name}_{prec}.npy"), R.raytrace(cs, world, seed, device=0, precision=prec))
+            np.save(os.path.join(out_dir, f"{_tag(name, kw)}_{prec}.npy"),
+                    R.raytrace(cs, world, seed, device=0, precision=prec))
 
 
 def main():
@@ -39,7 +46,8 @@ def main():
         subprocess.run([sys.executable, __file__, "--child", d], check=True, env=env, timeout=600)
         dirs[tag] = d
     res = {}
-    for name, _ in CASES:
+    for name, kw in CASES:
+        name = _tag(name, kw)
         for prec in ("f64", "f32"):
             a = np.load(os.path.join(dirs["base"], f"{name}_{prec}.npy"))
             b = np.load(os.path.join(dirs["exp"], f"{name}_{prec}.npy"))
