@@ -828,9 +828,16 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   // (pawn+fog 415 -> 385 ms; 30 % is no gain there); sphere-only leaves are cheapest tested all
   // together (demo1: 100 % best, 60 % +1 %)
   {
-    bool spheres_only = true;
-    for (int j = (int)prefix.size(); j < n && spheres_only; ++j)
-      spheres_only = sc->prims[order[j]].kind == RT_PRIM_SPHERE;
+    bool spheres_only = true, static_tris = true, static_spheres = true;
+    for (int j = (int)prefix.size(); j < n; ++j) {
+      const rt_prim& p = sc->prims[order[j]];
+      spheres_only = spheres_only && p.kind == RT_PRIM_SPHERE;
+      static_tris = static_tris && p.kind == RT_PRIM_TRIANGLE && p.motion < 0;
+      static_spheres = static_spheres && p.kind == RT_PRIM_SPHERE && p.motion < 0;
+    }
+    // the leaf tests of the BVH kernel specialised to one primitive class (rt_trace.h trav_round
+    // kLeaf): bunny-Cornell 144.0 -> 139.7 ms binary64, demo1 63.9 -> 61.6 (profiles/r3/agg)
+    S.leaf_kind = n == (int)prefix.size() ? 0 : static_tris ? 1 : static_spheres ? 2 : 0;
     S.leaf_exit_pct = spheres_only ? 100 : sc->n_media > 0 ? 55 : 25;
     if (const char* e = std::getenv("RT_AMD_LEAF_EXIT_PCT")) S.leaf_exit_pct = std::max(1, std::min(100, atoi(e)));
     // and the decoupled lane loop's exit (KernelParams::trav_exit_pct): pawn+fog 386 -> 376 ms at
@@ -842,7 +849,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   return RT_OK;
 }
 
-int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, bool inst) {
+int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, bool inst, int leaf_kind) {
   int v = flat ? RT_VAR_FLAT : RT_VAR_BVH;
   if (inst) return RT_VAR_BVH | RT_VAR_INST | (noise ? RT_VAR_NOISE : 0) | (n_media > 0 ? RT_VAR_MEDIA : 0) |
                    (mats ? RT_VAR_MATS : 0) | (tex ? RT_VAR_TEX : 0);  // two-level traversal: the decoupled BVH loop
@@ -851,8 +858,14 @@ int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, boo
     if (!flat && (f == RT_VAR_BVH_LOCKSTEP || f == RT_VAR_BVH)) v = f;  // flat scenes run on any variant
     if (flat && f >= RT_VAR_FLAT && f <= RT_VAR_BVH) v = f;
   }
+  // one-class BVH leaves: the decoupled kernel without media (the media kernels' leaves mix a
+  // medium boundary's class with the surfaces'; env RT_AMD_LEAF_KIND=0 keeps the generic test)
+  int leaf = 0;
+  if (v == RT_VAR_BVH && n_media == 0) leaf = leaf_kind == 1 ? RT_VAR_LEAF_TRI : leaf_kind == 2 ? RT_VAR_LEAF_SPHERE : 0;
+  if (const char* e = std::getenv("RT_AMD_LEAF_KIND"))
+    if (atoi(e) == 0) leaf = 0;
   return v | (noise ? RT_VAR_NOISE : 0) | (n_media > 0 ? RT_VAR_MEDIA : 0) | (mats ? RT_VAR_MATS : 0) |
-         (tex ? RT_VAR_TEX : 0);
+         (tex ? RT_VAR_TEX : 0) | leaf;
 }
 
 template <class R>

@@ -34,9 +34,7 @@
 #define RT_MAX_TARGETS 8
 #ifndef RT_LEAF_MAX
 #define RT_LEAF_MAX 8
-// small items per resident lane kept for the queue tail (rt_build.cpp rt_host_plan_work; 0: one
-// item size).  Cornell 600x600x200, same box (profiles/r2/items/): binary64 6.77 -> 6.63 ms at
-// 16 (8: 6.69, 32: 6.64, 64: 6.78); FP32 3.50 -> 3.46 at 32 (16: 3.49); 8-GPU shares unchanged
+#endif
 // Work-item claims: a wave takes RT_POOL consecutive ids per queue atomic (rt_render_kernel.h
 // WaveWork).  64 -> 128: Cornell 4.13 -> 4.04 ms (at 32 the head word saturates: 7.2 ms)
 #ifndef RT_POOL
@@ -60,12 +58,14 @@
 #ifndef RT_BIG_CHUNK_MAX
 #define RT_BIG_CHUNK_MAX 16  // samples per big work item at most (rt_build.cpp rt_host_plan_work; 38-48: Cornell f64 +1.5 %)
 #endif
+// small items per resident lane kept for the queue tail (rt_build.cpp rt_host_plan_work; 0: one
+// item size).  Cornell 600x600x200, same box (profiles/r2/items/): binary64 6.77 -> 6.63 ms at
+// 16 (8: 6.69, 32: 6.64, 64: 6.78); FP32 3.50 -> 3.46 at 32 (16: 3.49); 8-GPU shares unchanged
 #ifndef RT_TAIL_ITEMS_F64
 #define RT_TAIL_ITEMS_F64 16
 #endif
 #ifndef RT_TAIL_ITEMS_F32
 #define RT_TAIL_ITEMS_F32 32
-#endif
 #endif
 #define RT_LEAF_SHIFT 6       // leaf encoding ~(first << 6 | count - 1), count <= 64
 #define RT_FLAT_MAX 32        // a set of at most this many leaves is one flat leaf (no traversal)
@@ -97,10 +97,12 @@
 #define RT_VAR_MATS 16         // flag: materials beyond lightSource / pitchBlack / lambertian
 #define RT_VAR_TEX 32          // flag: some material reads a non-constant texture
 #define RT_VAR_INST 64         // flag: the scene has instances (two-level traversal; RT_VAR_BVH only)
+#define RT_VAR_LEAF_TRI 128    // flag: every BVH leaf record is a static triangle (RT_VAR_BVH, no media / instances)
+#define RT_VAR_LEAF_SPHERE 256 // flag: every BVH leaf record is a static sphere (idem)
 // workgroup size of a variant's render kernel
 inline int rt_block_of(int variant) { return (variant & RT_VAR_BASE) == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH; }
 // host choice of variant (rt_build.cpp); env RT_AMD_VARIANT overrides the base for experiments
-int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, bool inst = false);
+int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, bool inst = false, int leaf_kind = 0);
 
 #define RT_KIND_MASK 3
 #define RT_FLAG_MOTION 4
@@ -341,6 +343,7 @@ struct HostScene {
   int trav_exit_pct = 50;   // and its lane-loop exit (KernelParams::trav_exit_pct)
   bool full_mats = false;  // some material is not lightSource / pitchBlack / lambertian (RT_VAR_MATS)
   int n_instances = 0;     // two-level instancing (RT_VAR_INST)
+  int leaf_kind = 0;       // BVH leaves (after the prefix): 1 all static triangles, 2 all static spheres, 0 mixed
   template <class R>
   const HostArraysT<R>& arrays() const;
 };

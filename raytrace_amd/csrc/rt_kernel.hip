@@ -6,12 +6,13 @@
 // rt_render_kernel: a grid of exactly the resident workgroups (occupancy query), 256 lanes each,
 // instantiated per scene class (texture level, media, materials; see render_kernel_of).  Waves
 // start with a static pool of RT_POOL item ids and refill it with one returning atomicAdd on the
-// queue head (ballot the lanes that need work; ids are handed out in lane order), so
-// consecutive lanes take consecutive pixels (coherent primary rays).  Each lane keeps its
-// BVH traversal stack in LDS, laid out [depth][lane]: the 64 lanes of a wave touch 64
-// consecutive dwords (conflict-free).  The stack depth is the scene's BVH depth (dynamic LDS),
-// so shallow scenes are not occupancy-limited by LDS.  Finished items add their int64
-// fixed-point sums with 64-bit atomics (commutative: bit-exact for any schedule).
+// queue head (ballot the lanes that need work; ids are handed out in lane order); ids are
+// pixel-major, so a pool covers a few pixels (coherent primary rays) and its items' int64
+// fixed-point sums are added up per pixel in the wave's LDS slot before one 64-bit atomic per
+// word goes to HBM (commutative: bit-exact for any schedule; rt_render_kernel.h WaveWork).  Each
+// lane keeps its BVH traversal stack in LDS, laid out [depth][lane]: the 64 lanes of a wave touch
+// 64 consecutive dwords (conflict-free).  The stack depth is the scene's BVH depth (dynamic LDS),
+// so shallow scenes are not occupancy-limited by LDS.
 // No MFMA: the work is branchy scalar floating point, not a contraction.
 #define RT_F64 0
 #include "rt_render_kernel.h"

@@ -325,7 +325,7 @@ struct WaveWork {
 // commit-aggregation slots per wave and pixels per slot of a kernel class (rt_internal.h)
 #define RT_AGG_SLOTS_OF(kVar) ((kVar) == RT_VAR_FLAT ? RT_AGG_SLOTS_FLAT : RT_AGG_SLOTS_BVH)
 #define RT_AGG_PIX_OF(kVar) ((kVar) == RT_VAR_FLAT ? RT_AGG_PIX_FLAT : RT_AGG_PIX_BVH)
-template <int kVar, int kTex, bool kMedia, bool kMats, bool kInst>
+template <int kVar, int kTex, bool kMedia, bool kMats, bool kInst, int kLeaf>
 __global__ __launch_bounds__(kVar == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH)
 __attribute__((amdgpu_waves_per_eu(RT_WAVES_OF(kVar, kTex, kMedia, kMats))))
 void rt_render_kernel(KernelParams P) {
@@ -369,7 +369,7 @@ void rt_render_kernel(KernelParams P) {
     if constexpr (kVar == RT_VAR_BVH_LOCKSTEP)
       overflow = lane_loop_lockstep<false, kTex, kMedia, kMats>(P, work, W, P.prims, acc);
     else
-      overflow = lane_loop_bvh<kTex, kMedia, kMats, kInst>(P, work, W, P.prims, acc);
+      overflow = lane_loop_bvh<kTex, kMedia, kMats, kInst, kLeaf>(P, work, W, P.prims, acc);
     work.finish();
   }
   if (overflow) atomicOr(P.status, 1);
@@ -424,15 +424,20 @@ static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
 // (inlined everywhere it raises the register allocation of every scene's kernel: the Cornell
 // box is 4.8 % faster without the unused media code)
 typedef void (*render_fn)(KernelParams);
-template <int kVar, int kTex, bool kMedia, bool kInst>
+template <int kVar, int kTex, bool kMedia, bool kInst, int kLeaf>
 static render_fn render_kernel_mats(int variant) {
-  return (variant & RT_VAR_MATS) ? rt_render_kernel<kVar, kTex, kMedia, true, kInst>
-                                 : rt_render_kernel<kVar, kTex, kMedia, false, kInst>;
+  return (variant & RT_VAR_MATS) ? rt_render_kernel<kVar, kTex, kMedia, true, kInst, kLeaf>
+                                 : rt_render_kernel<kVar, kTex, kMedia, false, kInst, kLeaf>;
 }
 template <int kVar, int kTex, bool kInst>
 static render_fn render_kernel_media(int variant) {
-  return (variant & RT_VAR_MEDIA) ? render_kernel_mats<kVar, kTex, true, kInst>(variant)
-                                  : render_kernel_mats<kVar, kTex, false, kInst>(variant);
+  if (variant & RT_VAR_MEDIA) return render_kernel_mats<kVar, kTex, true, kInst, 0>(variant);
+  // one-class BVH leaves (RT_VAR_LEAF_*): the decoupled kernel without media or instances only
+  if constexpr (kVar == RT_VAR_BVH && !kInst) {
+    if (variant & RT_VAR_LEAF_TRI) return render_kernel_mats<kVar, kTex, false, kInst, 1>(variant);
+    if (variant & RT_VAR_LEAF_SPHERE) return render_kernel_mats<kVar, kTex, false, kInst, 2>(variant);
+  }
+  return render_kernel_mats<kVar, kTex, false, kInst, 0>(variant);
 }
 template <int kVar, bool kInst>
 static render_fn render_kernel_flags(int variant) {

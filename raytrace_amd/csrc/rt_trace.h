@@ -1,10 +1,11 @@
 // rt_trace.h — the per-lane path-tracing logic of the MI355X megakernel (rt_kernel.hip).
 //
 // Work decomposition: the frame (this shard's rows) x spp is cut into ITEMS = (tile pixel,
-// chunk of consecutive samples).  Lanes are persistent: a lane whose item is exhausted claims
-// the next item from its wave's pool, refilled from one of four queue head words (one
-// wave-aggregated atomic per 128 items; rt_render_kernel.h WaveWork), so every lane
-// stays busy until the queue drains and the tail is one chunk long.  Inside an item a lane
+// chunk of consecutive samples), numbered pixel-major.  Lanes are persistent: a lane whose item
+// is exhausted claims the next item from its wave's pool, refilled from one of four queue head
+// words (one wave-aggregated atomic per 128 items; rt_render_kernel.h WaveWork, which also sums a
+// pool's items per pixel in LDS before they reach HBM), so every lane stays busy until the queue
+// drains and the tail is one chunk long.  Inside an item a lane
 // regenerates paths: when a path terminates the next sample starts at once.  Per segment:
 //   1. closest hit: flat sets (class loops and box groups over wave-uniform records), or the
 //      surface set's large-primitive prefix then its BVH (stack in LDS, near child first,
@@ -1091,7 +1092,9 @@ RT_FN bool trav_done(const TravState& S) { return S.node == RT_EMPTY_ROOT && S.l
 // is moved to object space, RT_INST_EXIT is pushed and the object's BVH is traversed; popping
 // RT_INST_EXIT restores the world ray.  t is the same in both spaces (rigid), so the closest
 // hit's bound carries over; a parked leaf is tested before the ray changes space.
-template <bool kInst = false, class RC>
+// kLeaf: 0 generic leaf records; 1 / 2 every leaf record is a static triangle / sphere (one test,
+// no class dispatch or motion; a measured 2-4 % on the bunny and demo1 scenes)
+template <bool kInst = false, int kLeaf = 0, class RC>
 RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W, int& overflow RT_PROF_PARAM) {
   unsigned long long pf_c0 = RT_PROF_CLK();
   constexpr int kDone = RT_EMPTY_ROOT;
@@ -1254,8 +1257,15 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
     const int enc = ~S.leaf;
     const int first = enc >> RT_LEAF_SHIFT, count = (enc & ((1 << RT_LEAF_SHIFT) - 1)) + 1;
     for (int k = 0; k < count; ++k)
-      test_rec<false, kInst>(P, ld_rec(cf(P.prims) + 16 * (size_t)(first + k)), first + k, R, S.tmin, S.tmin_up, S.C,
-                             S.inst, S.ord_base);
+    {
+      const PrimRec r = ld_rec(cf(P.prims) + 16 * (size_t)(first + k));
+      if constexpr (kLeaf == 1)  // every leaf a static triangle (RT_VAR_LEAF_TRI)
+        test_static<RT_PRIM_CLASS_TRI, false>(r, R, S.tmin, S.tmin_up, S.C, first + k);
+      else if constexpr (kLeaf == 2)  // every leaf a static sphere (RT_VAR_LEAF_SPHERE)
+        test_static<RT_PRIM_CLASS_SPHERE, false>(r, R, S.tmin, S.tmin_up, S.C, first + k);
+      else
+        test_rec<false, kInst>(P, r, first + k, R, S.tmin, S.tmin_up, S.C, S.inst, S.ord_base);
+    }
 #ifdef RT_EXP_DOUBLE_LEAF  // ablation: every leaf tested twice (marginal cost of the leaf tests)
     for (int k = 0; k < count; ++k)
       test_rec(P, ld_rec(cf(P.prims) + 16 * (size_t)(first + k)), first + k, R, S.tmin,
@@ -1698,7 +1708,7 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Work& work, const Trav& TW, 
 // entering it, the second (Geometry.hs:306-328) — each starting inside the traversal loop as
 // soon as the previous one finishes.
 enum : int { ST_NEED_ITEM = 0, ST_NEED_SAMPLE = 1, ST_START_SEG = 2, ST_TRACE = 3, ST_SHADE = 4 };
-template <int kTex, bool kMedia, bool kMats, bool kInst, class Work, class AccT>
+template <int kTex, bool kMedia, bool kMats, bool kInst, int kLeaf, class Work, class AccT>
 RT_FN int lane_loop_bvh(const KernelParams& P, Work& work, const Trav& TW, const real* prims_, AccT& acc) {
   const cfp prims = cf(prims_);
   const int n_media = kMedia ? P.n_media : 0;  // media code only in the kMedia instantiations
@@ -1773,7 +1783,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Work& work, const Trav& TW, const
       RT_PROF_ADD(PF_TRACING, n_tr);
       RT_PROF_ADD(PF_LIVE, n_live);
       if (tr) {
-        trav_round<kInst>(P, R, S, TW, overflow RT_PROF_ARG);
+        trav_round<kInst, kLeaf>(P, R, S, TW, overflow RT_PROF_ARG);
         while (trav_done(S)) {
           int next_m = -1;  // medium whose first query starts next
           if (q == 0) {
@@ -1817,7 +1827,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Work& work, const Trav& TW, const
           }
           // a query over a set that is a single leaf (e.g. a fog sphere) is tested right away
           if (state != ST_TRACE || S.node != RT_EMPTY_ROOT) break;
-          trav_round<kInst>(P, R, S, TW, overflow RT_PROF_ARG);
+          trav_round<kInst, kLeaf>(P, R, S, TW, overflow RT_PROF_ARG);
         }
       }
     }

@@ -40,12 +40,16 @@ int run_loop(const RT_NS::KernelParams& P, int variant, G& g, const RT_NS::Trav&
   // the item sums through the device kernels' LDS accumulator (one lane: stride 1)
   unsigned long long words[6] = {0, 0, 0, 0, 0, 0};
   RT_NS::AccLds acc{words, 1};
-  if (variant & RT_VAR_INST) return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, true>(P, g, W, P.prims, acc);
+  if (variant & RT_VAR_INST) return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, true, 0>(P, g, W, P.prims, acc);
+  if ((variant & RT_VAR_BASE) == RT_VAR_BVH && !kMedia) {  // one-class leaves, as the device kernels
+    if (variant & RT_VAR_LEAF_TRI) return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, false, 1>(P, g, W, P.prims, acc);
+    if (variant & RT_VAR_LEAF_SPHERE) return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, false, 2>(P, g, W, P.prims, acc);
+  }
   switch (variant & RT_VAR_BASE) {
     case RT_VAR_FLAT: return RT_NS::lane_loop_lockstep<true, kTex, kMedia, kMats>(P, g, W, P.prims, acc);
     case RT_VAR_BVH_LOCKSTEP:
       return RT_NS::lane_loop_lockstep<false, kTex, kMedia, kMats>(P, g, W, P.prims, acc);
-    default: return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, false>(P, g, W, P.prims, acc);
+    default: return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, false, 0>(P, g, W, P.prims, acc);
   }
 }
 template <int kTex, class G>
@@ -105,7 +109,7 @@ int render(const HostScene& H, const rt_camera_settings* cs, uint64_t seed, cons
   for (int k = 0; k <= RT_MAX_MEDIA; ++k) P.flat_sets[k] = H.flat_sets[k];
   P.stack_depth = H.max_depth > 1 ? H.max_depth : 1;
   P.n_prims = H.n_prims;
-  const int variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex, H.n_instances > 0);
+  const int variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex, H.n_instances > 0, H.leaf_kind);
   rt_host_plan_work(P, 4096, (variant & RT_VAR_BASE) == RT_VAR_FLAT);
   P.trav_exit_pct = H.trav_exit_pct;
   if (chunk > 0) {

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Commit-aggregation session (round 3): GPU tests, image bit-identity against the previous kernel
 # build (raytrace_amd/_lib/exp/*.so), then kernel ms per config and precision for the in-tree
-# build with aggregation (agg), without it (RT_AMD_AGG=0: pixel-major ids only) and each exp lib.
+# build with aggregation (agg), without it (RT_AMD_AGG=0: pixel-major ids only) and each exp lib;
+# VARIANTS="name:ENV=v ..." replaces the two in-tree settings (one name:ENV pair per word).
 #   bash tools/sess_agg.sh <tag> ["<config> ..."] [precisions]
 set -o pipefail
 export TMPDIR=/tmp
@@ -26,8 +27,7 @@ run() {  # name lib-or-empty env...
 for rep in $(seq 1 ${REPS:-1}); do
 for p in $PRECS; do
   for c in $CFGS; do
-    run agg_r$rep "" RT_AMD_AGG=1
-    run noagg_r$rep "" RT_AMD_AGG=0
+    for v in ${VARIANTS:-"agg:RT_AMD_AGG=1" "noagg:RT_AMD_AGG=0"}; do run ${v%%:*}_r$rep "" ${v#*:}; done
     for lib in raytrace_amd/_lib/exp/*.so; do [ -e "$lib" ] && run $(basename $lib .so)_r$rep $lib RT_AMD_AGG=1; done
   done
 done

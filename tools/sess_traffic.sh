@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 TAG=$1; O=gpurun_out/$TAG; mkdir -p $O
 for cp in $2; do
   c=${cp%%:*}; p=${cp#*:}
-  for lib in "" raytrace_amd/_lib/exp/*.so; do
+  for lib in "" ${LIBS:-raytrace_amd/_lib/exp/*.so}; do
     if [ -n "$lib" ]; then [ -e "$lib" ] || continue; export RT_AMD_LIB=$PWD/$lib; nm=$(basename $lib .so); else unset RT_AMD_LIB; nm=intree; fi
     for ctr in FETCH_SIZE WRITE_SIZE; do
       timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $O/${c}_${p}_${nm}_$ctr -o run -- \
