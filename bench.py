@@ -290,9 +290,12 @@ def main():
     def measure(precision):
         """Warm up, then time exactly args.steps frames in `precision`; returns the rank's timings."""
         dtype = torch.float64 if precision == "f64" else torch.float32
-        # two frame buffers: frame i+1 renders while the RCCL gather of frame i is in flight on the
-        # collective's own stream (the compute stream waits for gather i-1 before reusing its tile)
-        nbuf = 2 if n > 1 or args.streams > 1 else 1
+        # frame buffers: frame i+1 renders while the RCCL gather of frame i is in flight on the
+        # collective's own stream (the compute stream waits for the gather that last read a tile
+        # before reusing it).  Two streams at N > 1 take three buffers: gather i starts only after
+        # frame i's resolve, which queues behind frame i+1's persistent grid (DESIGN §6), so with two
+        # buffers frame i+2 would wait for that gather and leave frame i+1's tail alone on the CUs
+        nbuf = (3 if args.streams > 1 else 2) if n > 1 else (2 if args.streams > 1 else 1)
         tiles = [torch.empty((rows, w, 3), dtype=dtype, device=dev) for _ in range(nbuf)]
         gathered = [torch.empty((n * rows, w, 3), dtype=dtype, device=dev) for _ in range(nbuf)] if n > 1 else None
         works = [None] * nbuf

@@ -1087,6 +1087,15 @@ RT_FN void trav_begin(TravState& S, int root, real tmin) {
 }
 RT_FN bool trav_done(const TravState& S) { return S.node == RT_EMPTY_ROOT && S.leaf == 0; }
 
+#ifndef RT_NODE_FETCH_UNIFORM  // 1: measured slower (pawn+fog +8.5 % FP32, whose BVH is mostly staged)
+#define RT_NODE_FETCH_UNIFORM 0
+#endif
+// FP32 kernels read global nodes at a 32-bit offset from the uniform base (bunny-Cornell -0.3 %,
+// demo1 -1.5 %, pawn+fog -1.0 %); the binary64 kernels keep 64-bit addresses (demo1 +2.4 % with
+// the offsets, bunny and pawn+fog -0.9 %: profiles/r3/fetch)
+#ifndef RT_NODE_SADDR
+#define RT_NODE_SADDR (!RT_F64)
+#endif
 // One while-while round: descend until this lane (and the wave) holds a leaf, then test leaves.
 // kInst (two-level instancing): a child RT_INST_FLAG | k enters placement k — the lane's ray R
 // is moved to object space, RT_INST_EXIT is pushed and the object's BVH is traversed; popping
@@ -1151,7 +1160,15 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
     v4f n0, n1, n2;
     int cl, cr;
     const int node = S.node;
-    if (node < P.lds_nodes) {  // top levels of the surface BVH, staged in LDS per workgroup
+#if RT_NODE_FETCH_UNIFORM
+    // wave-uniform source: LDS only when every stepping lane's node is staged, else every lane reads
+    // global memory (the staged nodes are there too) — a mixed wave would run both paths, the LDS
+    // reads waiting for the global loads that target the same registers
+    const bool from_lds = !RT_ANY(node >= P.lds_nodes);
+#else
+    const bool from_lds = node < P.lds_nodes;
+#endif
+    if (from_lds) {  // top levels of the surface BVH, staged in LDS per workgroup
       const v4f* nd = W.lds_nodes + 4 * node;
       n0 = nd[0];
       n1 = nd[1];
@@ -1159,7 +1176,13 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
       cl = RT_F2I(nd[3].x);
       cr = RT_F2I(nd[3].y);
     } else {
+#if RT_NODE_SADDR
+      // a 32-bit byte offset from the uniform base (node < 2^25): the loads take the scalar-base +
+      // vector-offset form, no 64-bit address arithmetic per lane
+      cfpf nd = (cfpf)((const RT_CAS char*)P.nodes + ((uint32_t)node << 6));
+#else
       cfpf nd = (cfpf)P.nodes + 16 * (size_t)node;
+#endif
       n0 = ldc4f(nd);
       n1 = ldc4f(nd + 4);
       n2 = ldc4f(nd + 8);
