@@ -832,8 +832,17 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     for (int j = (int)prefix.size(); j < n; ++j) {
       const rt_prim& p = sc->prims[order[j]];
       spheres_only = spheres_only && p.kind == RT_PRIM_SPHERE;
-      static_tris = static_tris && p.kind == RT_PRIM_TRIANGLE && p.motion < 0;
-      static_spheres = static_spheres && p.kind == RT_PRIM_SPHERE && p.motion < 0;
+    }
+    // one-class leaves: the classes of the leaves the traversal reaches through BVH nodes (the
+    // surface set, and the media sets with a BVH); a medium set that is a single leaf (a fog
+    // sphere) is tested by the generic test (rt_trace.h test_leaf_generic)
+    for (int s = 0; s < n_sets; ++s) {
+      if (s > 0 && roots[s] < 0) continue;
+      for (int j = set_begin[s]; j < set_begin[s + 1]; ++j) {
+        const rt_prim& p = sc->prims[order[j]];
+        static_tris = static_tris && p.kind == RT_PRIM_TRIANGLE && p.motion < 0;
+        static_spheres = static_spheres && p.kind == RT_PRIM_SPHERE && p.motion < 0;
+      }
     }
     // the leaf tests of the BVH kernel specialised to one primitive class (rt_trace.h trav_round
     // kLeaf): bunny-Cornell 144.0 -> 139.7 ms binary64, demo1 63.9 -> 61.6 (profiles/r3/agg)
@@ -858,10 +867,11 @@ int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, boo
     if (!flat && (f == RT_VAR_BVH_LOCKSTEP || f == RT_VAR_BVH)) v = f;  // flat scenes run on any variant
     if (flat && f >= RT_VAR_FLAT && f <= RT_VAR_BVH) v = f;
   }
-  // one-class BVH leaves: the decoupled kernel without media (the media kernels' leaves mix a
-  // medium boundary's class with the surfaces'; env RT_AMD_LEAF_KIND=0 keeps the generic test)
+  // one-class BVH leaves: the decoupled kernel (leaf_kind covers the leaves below BVH nodes of the
+  // surface and media sets; the kernel dispatch keeps the generic test where no one-class
+  // instantiation exists; env RT_AMD_LEAF_KIND=0 keeps the generic test)
   int leaf = 0;
-  if (v == RT_VAR_BVH && n_media == 0) leaf = leaf_kind == 1 ? RT_VAR_LEAF_TRI : leaf_kind == 2 ? RT_VAR_LEAF_SPHERE : 0;
+  if (v == RT_VAR_BVH) leaf = leaf_kind == 1 ? RT_VAR_LEAF_TRI : leaf_kind == 2 ? RT_VAR_LEAF_SPHERE : 0;
   if (const char* e = std::getenv("RT_AMD_LEAF_KIND"))
     if (atoi(e) == 0) leaf = 0;
   return v | (noise ? RT_VAR_NOISE : 0) | (n_media > 0 ? RT_VAR_MEDIA : 0) | (mats ? RT_VAR_MATS : 0) |

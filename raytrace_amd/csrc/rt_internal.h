@@ -97,8 +97,8 @@
 #define RT_VAR_MATS 16         // flag: materials beyond lightSource / pitchBlack / lambertian
 #define RT_VAR_TEX 32          // flag: some material reads a non-constant texture
 #define RT_VAR_INST 64         // flag: the scene has instances (two-level traversal; RT_VAR_BVH only)
-#define RT_VAR_LEAF_TRI 128    // flag: every BVH leaf record is a static triangle (RT_VAR_BVH, no media / instances)
-#define RT_VAR_LEAF_SPHERE 256 // flag: every BVH leaf record is a static sphere (idem)
+#define RT_VAR_LEAF_TRI 128    // flag: every BVH leaf below a BVH node is a static triangle (RT_VAR_BVH, no instances)
+#define RT_VAR_LEAF_SPHERE 256 // flag: ... a static sphere (idem; kernels without media only)
 // workgroup size of a variant's render kernel
 inline int rt_block_of(int variant) { return (variant & RT_VAR_BASE) == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH; }
 // host choice of variant (rt_build.cpp); env RT_AMD_VARIANT overrides the base for experiments

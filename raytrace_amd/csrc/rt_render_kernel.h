@@ -424,6 +424,9 @@ static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
 // (inlined everywhere it raises the register allocation of every scene's kernel: the Cornell
 // box is 4.8 % faster without the unused media code)
 typedef void (*render_fn)(KernelParams);
+#ifndef RT_LEAF_MEDIA
+#define RT_LEAF_MEDIA 1
+#endif
 template <int kVar, int kTex, bool kMedia, bool kInst, int kLeaf>
 static render_fn render_kernel_mats(int variant) {
   return (variant & RT_VAR_MATS) ? rt_render_kernel<kVar, kTex, kMedia, true, kInst, kLeaf>
@@ -431,8 +434,13 @@ static render_fn render_kernel_mats(int variant) {
 }
 template <int kVar, int kTex, bool kInst>
 static render_fn render_kernel_media(int variant) {
-  if (variant & RT_VAR_MEDIA) return render_kernel_mats<kVar, kTex, true, kInst, 0>(variant);
-  // one-class BVH leaves (RT_VAR_LEAF_*): the decoupled kernel without media or instances only
+  // one-class BVH leaves (RT_VAR_LEAF_*): the decoupled kernel without instances; with media,
+  // triangle leaves and constant textures only (pawn+fog)
+  if (variant & RT_VAR_MEDIA) {
+    if constexpr (kVar == RT_VAR_BVH && !kInst && kTex == 0 && RT_LEAF_MEDIA)
+      if (variant & RT_VAR_LEAF_TRI) return render_kernel_mats<kVar, kTex, true, kInst, 1>(variant);
+    return render_kernel_mats<kVar, kTex, true, kInst, 0>(variant);
+  }
   if constexpr (kVar == RT_VAR_BVH && !kInst) {
     if (variant & RT_VAR_LEAF_TRI) return render_kernel_mats<kVar, kTex, false, kInst, 1>(variant);
     if (variant & RT_VAR_LEAF_SPHERE) return render_kernel_mats<kVar, kTex, false, kInst, 2>(variant);

@@ -1305,6 +1305,19 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
   (void)pf_c1;
 }
 
+// A query whose set is one leaf (trav_begin parked it): its records by the generic test.
+template <bool kInst, class RC>
+RT_FN void test_leaf_generic(const KernelParams& P, RC& R, TravState& S) {
+  while (S.leaf < 0) {
+    const int enc = ~S.leaf;
+    const int first = enc >> RT_LEAF_SHIFT, count = (enc & ((1 << RT_LEAF_SHIFT) - 1)) + 1;
+    for (int k = 0; k < count; ++k)
+      test_rec<false, kInst>(P, ld_rec(cf(P.prims) + 16 * (size_t)(first + k)), first + k, R, S.tmin, S.tmin_up, S.C,
+                             S.inst, S.ord_base);
+    S.leaf = 0;
+  }
+}
+
 // kFlat: the set is one flat leaf (rt_internal.h DevFlatSet); every lane walks the same
 // records in the same order, so the loops are coherent and the records are scalar loads.
 template <>
@@ -1848,9 +1861,14 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Work& work, const Trav& TW, const
               state = ST_SHADE;
             }
           }
-          // a query over a set that is a single leaf (e.g. a fog sphere) is tested right away
+          // a query over a set that is a single leaf (e.g. a fog sphere) is tested right away;
+          // with one-class leaves by the generic test (the host checks only the classes of the
+          // leaves below BVH nodes: a single-leaf medium set may be any class, rt_build.cpp)
           if (state != ST_TRACE || S.node != RT_EMPTY_ROOT) break;
-          trav_round<kInst, kLeaf>(P, R, S, TW, overflow RT_PROF_ARG);
+          if constexpr (kLeaf != 0)
+            test_leaf_generic<kInst>(P, R, S);
+          else
+            trav_round<kInst, kLeaf>(P, R, S, TW, overflow RT_PROF_ARG);
         }
       }
     }

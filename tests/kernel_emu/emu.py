@@ -52,16 +52,17 @@ def render(settings, world, seed, n_shards=1, shard=0, row_block=4, nthreads=Non
 
 
 def scene_info(world):
-    """n_nodes, surface_nodes, max_depth, n_prims, flat, box groups and surface-prefix primitives of
-    the host build of `world`."""
+    """n_nodes, surface_nodes, max_depth, n_prims, flat, box groups, surface-prefix primitives and
+    the one-class leaf kind (1 static triangles, 2 static spheres, 0 mixed) of the host build of
+    `world`."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
     from raytrace_amd import _lib as R
     from raytrace_amd.scene import FlatScene, flatten
     flat = world if isinstance(world, FlatScene) else flatten(world)
     sc = R.scene_struct(flat)
-    info = np.zeros(7, np.int32)
+    info = np.zeros(8, np.int32)
     rc = lib().rt_emu_scene_info(ctypes.byref(sc), info.ctypes.data_as(ctypes.c_void_p))
     if rc != 0:
         raise RuntimeError(f"rt_emu_scene_info failed {rc}: {lib().rt_emu_last_error().decode()}")
-    return dict(zip(["n_nodes", "surface_nodes", "max_depth", "n_prims", "flat", "boxes", "prefix"], info.tolist()))
+    return dict(zip(["n_nodes", "surface_nodes", "max_depth", "n_prims", "flat", "boxes", "prefix", "leaf_kind"], info.tolist()))

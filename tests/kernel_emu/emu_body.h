@@ -41,9 +41,10 @@ int run_loop(const RT_NS::KernelParams& P, int variant, G& g, const RT_NS::Trav&
   unsigned long long words[6] = {0, 0, 0, 0, 0, 0};
   RT_NS::AccLds acc{words, 1};
   if (variant & RT_VAR_INST) return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, true, 0>(P, g, W, P.prims, acc);
-  if ((variant & RT_VAR_BASE) == RT_VAR_BVH && !kMedia) {  // one-class leaves, as the device kernels
+  if ((variant & RT_VAR_BASE) == RT_VAR_BVH) {  // one-class leaves, as the device kernels
     if (variant & RT_VAR_LEAF_TRI) return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, false, 1>(P, g, W, P.prims, acc);
-    if (variant & RT_VAR_LEAF_SPHERE) return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, false, 2>(P, g, W, P.prims, acc);
+    if ((variant & RT_VAR_LEAF_SPHERE) && !kMedia)
+      return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, false, 2>(P, g, W, P.prims, acc);
   }
   switch (variant & RT_VAR_BASE) {
     case RT_VAR_FLAT: return RT_NS::lane_loop_lockstep<true, kTex, kMedia, kMats>(P, g, W, P.prims, acc);

@@ -100,6 +100,7 @@ int rt_emu_scene_info(const rt_scene* sc, int* info) {
       for (int f = 0; f < 6; ++f) pre += ((H.f32.boxes[b].ord_code >> (5 * f)) & 31) != RT_BOX_NO_FACE;
   }
   info[6] = pre;
+  info[7] = H.leaf_kind;
   return RT_OK;
 }
 }

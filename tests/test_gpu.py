@@ -269,12 +269,13 @@ def test_commit_aggregation_is_exact(gpu, monkeypatch, name, precision):
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
-@pytest.mark.parametrize("name", ["bunny_cornell", "demo1"])
+@pytest.mark.parametrize("name", ["bunny_cornell", "demo1", "pawn_fog"])
 def test_one_class_leaf_kernels_are_exact(gpu, monkeypatch, name, precision):
     """BVH kernels whose leaf test is specialised to the scene's one primitive class (RT_VAR_LEAF_TRI
-    for the bunny, RT_VAR_LEAF_SPHERE for demo1) against the generic leaf test: the same
+    for the bunny and for pawn+fog — its media kernel, the fog sphere a single-leaf medium set
+    tested generically — RT_VAR_LEAF_SPHERE for demo1) against the generic leaf test: the same
     arithmetic per primitive, so bit-identical images."""
-    fn = {"bunny_cornell": scenes.bunny_cornell, "demo1": scenes.demo1}[name]
+    fn = {"bunny_cornell": scenes.bunny_cornell, "demo1": scenes.demo1, "pawn_fog": scenes.pawn_fog}[name]
     cs, world, seed = fn(width=96, spp=16)
     a = R.raytrace(cs, world, seed, precision=precision)
     monkeypatch.setenv("RT_AMD_LEAF_KIND", "0")

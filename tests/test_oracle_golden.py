@@ -191,6 +191,21 @@ def test_large_primitive_prefix_is_exact(emu_mod, monkeypatch, variant, name):
     assert ca["bvh_nodes"] < cb["bvh_nodes"]
 
 
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("name,kind", [("bunny_cornell", 1), ("demo1", 2), ("pawn_fog", 1), ("pawn_test", 1), ("bunny_instances", 0)])
+def test_one_class_leaves_are_exact(emu_mod, monkeypatch, name, kind, precision):
+    """The host picks one-class leaf kernels from the leaves below BVH nodes (pawn+fog: the pawn's
+    triangles in the surface and medium sets; its fog sphere is a single-leaf medium set, tested
+    generically), and they render the generic kernel's image bit for bit."""
+    cs, world, seed = scenes.CONFIGS[name](width=40, spp=4)
+    assert emu_mod.scene_info(world)["leaf_kind"] == kind
+    a = emu_mod.render(cs, world, seed, precision=precision)
+    monkeypatch.setenv("RT_AMD_LEAF_KIND", "0")
+    b = emu_mod.render(cs, world, seed, precision=precision)
+    assert np.isfinite(a).all() and a.mean() > 0
+    assert np.array_equal(a, b, equal_nan=True)
+
+
 @pytest.mark.parametrize("name", ["cornell", "box_gallery", "bunny_cornell"])
 def test_box_groups_match_per_face_tests(oracle_mod, emu_mod, monkeypatch, name):
     """Cuboid faces and the Cornell walls tested as box groups (one slab test per box, DevBox)
