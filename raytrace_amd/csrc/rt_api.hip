@@ -155,12 +155,14 @@ int ensure_precision(const rt_device_scene* s) {
   if ((s->variant & RT_VAR_BASE) != RT_VAR_FLAT) {
     // stage as many top (breadth-first) surface nodes as fit beside the lanes' item sums and
     // stacks in the workgroup's share of the CU's 160 KB LDS at the kernel's occupancy (1 KB
-    // granules; 4 waves per workgroup: one workgroup per SIMD wave slot); env RT_AMD_LDS_NODES
-    // caps it (0 disables, for experiments)
+    // granules; 4 x waves-per-SIMD waves per CU, `block` threads per workgroup); env
+    // RT_AMD_LDS_NODES caps it (0 disables, for experiments)
     const int waves = std::max(1, rt_render_waves((const KernelParamsT<R>*)nullptr, s->variant));
-    const int budget = (163840 / waves / 1024) * 1024 - 1024;
+    const int block = rt_render_block((const KernelParamsT<R>*)nullptr, s->variant);
+    const int per_cu = std::max(1, 4 * waves * 64 / block);
+    const int budget = (163840 / per_cu / 1024) * 1024 - 1024;
     const int used = rt_render_acc_lds((const KernelParamsT<R>*)nullptr, s->variant) +
-                     (s->stack_depth + 1) * RT_BLOCK_BVH * (int)sizeof(int);
+                     (s->stack_depth + 1) * block * (int)sizeof(int);
     A.lds_nodes = std::max(0, std::min(s->host->surface_nodes, (budget - used) / 64));
     if (const char* e = std::getenv("RT_AMD_LDS_NODES")) A.lds_nodes = std::min(A.lds_nodes, std::max(0, atoi(e)));
   }
@@ -211,7 +213,8 @@ int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_
   P.stack_depth = s->stack_depth;
   P.lds_nodes = A.lds_nodes;
   P.n_prims = s->n_prims;
-  rt_host_plan_work(P, (long long)A.resident_blocks * rt_block_of(s->variant), (s->variant & RT_VAR_BASE) == RT_VAR_FLAT);
+  rt_host_plan_work(P, (long long)A.resident_blocks * rt_render_block((const KernelParamsT<R>*)nullptr, s->variant),
+                    (s->variant & RT_VAR_BASE) == RT_VAR_FLAT);
   P.trav_exit_pct = s->trav_exit_pct;
   HIP_TRY(hipSetDevice(s->device));
   // stream-ordered workspace: fixed-point sums, NaN flags, queue counter (graph-capturable)

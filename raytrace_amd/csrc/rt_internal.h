@@ -26,7 +26,7 @@
 #define RT_BLOCK 256          // flat kernel workgroup
 #endif
 #ifndef RT_BLOCK_BVH
-#define RT_BLOCK_BVH 256      // BVH kernel workgroup (its lanes share one LDS copy of the top nodes)
+#define RT_BLOCK_BVH 256      // BVH kernel workgroup at 5 waves/SIMD (others: rt_render_kernel.h RT_BLOCK_OF)
 #endif
 #define RT_STACK_DEPTH 64     // deepest BVH accepted: the LDS stack is sized by the scene's actual depth (deep
                               // trees lower occupancy instead of failing)
@@ -100,7 +100,6 @@
 #define RT_VAR_LEAF_TRI 128    // flag: every BVH leaf below a BVH node is a static triangle (RT_VAR_BVH, no instances)
 #define RT_VAR_LEAF_SPHERE 256 // flag: ... a static sphere (idem; kernels without media only)
 // workgroup size of a variant's render kernel
-inline int rt_block_of(int variant) { return (variant & RT_VAR_BASE) == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH; }
 // host choice of variant (rt_build.cpp); env RT_AMD_VARIANT overrides the base for experiments
 int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, bool inst = false, int leaf_kind = 0);
 
@@ -378,6 +377,8 @@ int rt_render_resident_blocks(const KernelParams*, int device, int stack_depth, 
 int rt_render_resident_blocks(const KernelParams64*, int device, int stack_depth, int variant, int lds_nodes);
 int rt_render_waves(const KernelParams*, int variant);
 int rt_render_waves(const KernelParams64*, int variant);
+int rt_render_block(const KernelParams*, int variant);  // the workgroup size of a variant's kernel
+int rt_render_block(const KernelParams64*, int variant);
 int rt_render_acc_lds(const KernelParams*, int variant);
 int rt_render_acc_lds(const KernelParams64*, int variant);
 int rt_launch_render(const KernelParams& p, int grid_blocks, int variant, void* stream);

@@ -322,15 +322,27 @@ struct WaveWork {
   ((kVar) == RT_VAR_FLAT ? ((kTex) == 2 ? RT_WAVES_FLAT_NOISE : (kTex) == 0 ? RT_WAVES_FLAT_TEX0 : RT_WAVES_FLAT) \
                          : ((kTex) == 0 && !(kMedia) ? RT_WAVES_BVH_LITE : RT_WAVES_BVH))
 #endif
+// BVH workgroup size of a kernel class: each workgroup stages its own LDS copy of the top BVH
+// nodes, so the fewer workgroups share a CU the more nodes each copy holds (pawn+fog and demo1
+// gain 6-13 % from staging).  The largest workgroup whose waves split evenly over the
+// CU's 4 SIMDs at the kernel's occupancy W (waves per SIMD): W = 3 -> 768 threads (one per CU),
+// 4 -> 512 (two), 6 -> 768 (two); W = 5 keeps 256 (five).  RT_BIG_WG=0: 256 everywhere.
+#ifndef RT_BIG_WG
+#define RT_BIG_WG 1
+#endif
+#define RT_BLOCK_BVH_OF(w) (RT_BIG_WG && ((w) == 3 || (w) == 6) ? 768 : RT_BIG_WG && (w) == 4 ? 512 : RT_BLOCK_BVH)
+#define RT_BLOCK_OF(kVar, kTex, kMedia, kMats) \
+  ((kVar) == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH_OF(RT_WAVES_OF(kVar, kTex, kMedia, kMats)))
 // commit-aggregation slots per wave and pixels per slot of a kernel class (rt_internal.h)
 #define RT_AGG_SLOTS_OF(kVar) ((kVar) == RT_VAR_FLAT ? RT_AGG_SLOTS_FLAT : RT_AGG_SLOTS_BVH)
 #define RT_AGG_PIX_OF(kVar) ((kVar) == RT_VAR_FLAT ? RT_AGG_PIX_FLAT : RT_AGG_PIX_BVH)
 template <int kVar, int kTex, bool kMedia, bool kMats, bool kInst, int kLeaf>
-__global__ __launch_bounds__(kVar == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH)
+__global__ __launch_bounds__(RT_BLOCK_OF(kVar, kTex, kMedia, kMats))
 __attribute__((amdgpu_waves_per_eu(RT_WAVES_OF(kVar, kTex, kMedia, kMats))))
 void rt_render_kernel(KernelParams P) {
   extern __shared__ int smem[];
   constexpr int kSlots = RT_AGG_SLOTS_OF(kVar), kPix = RT_AGG_PIX_OF(kVar);
+  constexpr int kBlock = RT_BLOCK_OF(kVar, kTex, kMedia, kMats);
   constexpr int kAggBytes = AggGeom<kSlots, kPix>::kWaveBytes;
   const int waves = (int)(gridDim.x * (blockDim.x / 64));
   // wave-uniform (readfirstlane: the compiler cannot tell that threadIdx.x / 64 is), so the work
@@ -339,7 +351,7 @@ void rt_render_kernel(KernelParams P) {
   const int wave = (int)blockIdx.x * (int)(blockDim.x / 64) + wave_in_block;
   int overflow;
   // LDS: the lanes' item sums [RT_ACC_WORDS][block] (rt_trace.h AccLds; BVH kernels), the waves'
-  // commit-aggregation slots (kAggBytes each), then (BVH kernels) [stack_depth + 1][RT_BLOCK_BVH]
+  // commit-aggregation slots (kAggBytes each), then (BVH kernels) [stack_depth + 1][kBlock]
   // stack words (the last row a spare write target) and the top P.lds_nodes BVH nodes (64 B each)
   using AccT = typename std::conditional<RT_ACC_LDS_OF(kVar, kMedia), AccLds, Acc>::type;
   AccT acc;
@@ -357,15 +369,15 @@ void rt_render_kernel(KernelParams P) {
     overflow = lane_loop_lockstep<true, kTex, kMedia, kMats>(P, work, Trav{nullptr, 0, nullptr}, P.prims, acc);
     work.finish();
   } else {
-    v4f* lds_nodes = reinterpret_cast<v4f*>(smem_rest + (P.stack_depth + 1) * RT_BLOCK_BVH);
+    v4f* lds_nodes = reinterpret_cast<v4f*>(smem_rest + (P.stack_depth + 1) * kBlock);
     const float4* src = reinterpret_cast<const float4*>(P.nodes);
-    for (int i = threadIdx.x; i < 4 * P.lds_nodes; i += RT_BLOCK_BVH) {
+    for (int i = threadIdx.x; i < 4 * P.lds_nodes; i += kBlock) {
       const float4 q = src[i];
       lds_nodes[i] = v4f{q.x, q.y, q.z, q.w};
     }
     __syncthreads();
     WaveWork<kSlots, kPix> work(P, wave, waves, agg);
-    const Trav W{smem_rest + threadIdx.x, RT_BLOCK_BVH, lds_nodes};
+    const Trav W{smem_rest + threadIdx.x, kBlock, lds_nodes};
     if constexpr (kVar == RT_VAR_BVH_LOCKSTEP)
       overflow = lane_loop_lockstep<false, kTex, kMedia, kMats>(P, work, W, P.prims, acc);
     else
@@ -399,22 +411,30 @@ __global__ __launch_bounds__(256) void rt_resolve_kernel(const long long* __rest
 #endif
 }
 
+// the workgroup size of a variant's kernel (RT_BLOCK_OF of its class)
+static int render_block(int variant) {
+  const bool flat = (variant & RT_VAR_BASE) == RT_VAR_FLAT;
+  const int tex = (variant & RT_VAR_NOISE) ? 2 : (variant & RT_VAR_TEX) ? 1 : 0;
+  const bool media = (variant & RT_VAR_MEDIA) != 0, mats = (variant & RT_VAR_MATS) != 0;
+  (void)mats;
+  return RT_BLOCK_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats);
+}
 static bool acc_in_lds(int variant) {
   return RT_ACC_LDS_OF((variant & RT_VAR_BASE) == RT_VAR_FLAT ? RT_VAR_FLAT : RT_VAR_BVH, (variant & RT_VAR_MEDIA) != 0);
 }
 // LDS besides the stacks and the staged nodes: the lanes' item sums and the aggregation slots
 static size_t render_fixed_lds(int variant) {
   const bool flat = (variant & RT_VAR_BASE) == RT_VAR_FLAT;
-  const size_t acc = acc_in_lds(variant) ? (size_t)RT_ACC_WORDS(real) * 8 * rt_block_of(variant) : 0;
+  const size_t acc = acc_in_lds(variant) ? (size_t)RT_ACC_WORDS(real) * 8 * render_block(variant) : 0;
   const size_t agg = (size_t)(flat ? AggGeom<RT_AGG_SLOTS_FLAT, RT_AGG_PIX_FLAT>::kWaveBytes
                                    : AggGeom<RT_AGG_SLOTS_BVH, RT_AGG_PIX_BVH>::kWaveBytes) *
-                     (rt_block_of(variant) / 64);
+                     (render_block(variant) / 64);
   return acc + agg;
 }
 static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
   return render_fixed_lds(variant) + ((variant & RT_VAR_BASE) == RT_VAR_FLAT
                     ? 0
-                    : (size_t)(stack_depth + 1) * RT_BLOCK_BVH * sizeof(int) + (size_t)lds_nodes * 64);
+                    : (size_t)(stack_depth + 1) * render_block(variant) * sizeof(int) + (size_t)lds_nodes * 64);
 }
 
 // the kernel instantiation of a variant code (base variant | RT_VAR_TEX | RT_VAR_NOISE |
@@ -473,7 +493,7 @@ int rt_render_resident_blocks(const KernelParamsT<RT_NS::real>*, int device, int
   if (lds > 65536 && hipFuncSetAttribute((const void*)render_kernel_of(variant),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -1;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_kernel_of(variant), rt_block_of(variant), lds);
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_kernel_of(variant), render_block(variant), lds);
   if (e != hipSuccess) return -1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return -1;
   if (per_cu < 1) per_cu = 1;
@@ -490,6 +510,7 @@ int rt_render_waves(const KernelParamsT<RT_NS::real>*, int variant) {
   (void)mats;  // the FP32 occupancy table does not depend on the material set
   return RT_WAVES_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats);
 }
+int rt_render_block(const KernelParamsT<RT_NS::real>*, int variant) { return RT_NS::render_block(variant); }
 int rt_render_acc_lds(const KernelParamsT<RT_NS::real>*, int variant) {
   return (int)RT_NS::render_fixed_lds(variant);
 }
@@ -497,7 +518,7 @@ int rt_render_acc_lds(const KernelParamsT<RT_NS::real>*, int variant) {
 int rt_launch_render(const KernelParamsT<RT_NS::real>& p, int grid_blocks, int variant, void* stream) {
   using namespace RT_NS;
   if (p.n_items <= 0 || grid_blocks <= 0) return 0;
-  const int block = rt_block_of(variant);
+  const int block = render_block(variant);
   long long need = ((long long)p.n_items + block - 1) / block;
   int grid = need < grid_blocks ? (int)need : grid_blocks;
   size_t lds = render_lds_bytes(p.stack_depth, variant, p.lds_nodes);
