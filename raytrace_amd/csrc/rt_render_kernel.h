@@ -330,7 +330,9 @@ struct WaveWork {
 #ifndef RT_BIG_WG
 #define RT_BIG_WG 1
 #endif
+#ifndef RT_BLOCK_BVH_OF
 #define RT_BLOCK_BVH_OF(w) (RT_BIG_WG && ((w) == 3 || (w) == 6) ? 768 : RT_BIG_WG && (w) == 4 ? 512 : RT_BLOCK_BVH)
+#endif
 #define RT_BLOCK_OF(kVar, kTex, kMedia, kMats) \
   ((kVar) == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH_OF(RT_WAVES_OF(kVar, kTex, kMedia, kMats)))
 // commit-aggregation slots per wave and pixels per slot of a kernel class (rt_internal.h)
