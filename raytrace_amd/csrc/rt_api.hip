@@ -102,7 +102,7 @@ struct rt_device_scene {
   mutable DevArrays<float> f32;
   mutable DevArrays<double> f64;
   mutable bool have_f32 = false, have_f64 = false;
-  int leaf_exit_pct = 100;
+  int leaf_exit_pct = 100, leaf_exit_pct64 = 100;
   int trav_exit_pct = 50;
   int surface_root = RT_EMPTY_ROOT;
   int n_media = 0;
@@ -205,7 +205,7 @@ int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_
   P.status = s->status;
   P.out = d_out;
   P.surface_root = s->surface_root;
-  P.leaf_exit_pct = s->leaf_exit_pct;
+  P.leaf_exit_pct = sizeof(R) == 8 ? s->leaf_exit_pct64 : s->leaf_exit_pct;
   P.surface_prefix = (s->variant & RT_VAR_BASE) != RT_VAR_FLAT && s->n_nodes > 0 ? 1 : 0;
   P.n_media = s->n_media;
   for (int k = 0; k < s->n_media; ++k) P.media[k] = A.media[k];
@@ -289,6 +289,7 @@ int upload_common(const std::shared_ptr<const HostScene>& Hp, int device, rt_dev
   }
   s->surface_root = H.surface_root;
   s->leaf_exit_pct = H.leaf_exit_pct;
+  s->leaf_exit_pct64 = H.leaf_exit_pct64;
   s->trav_exit_pct = H.trav_exit_pct;
   s->n_media = H.n_media;
   for (int k = 0; k <= RT_MAX_MEDIA; ++k) s->flat_sets[k] = H.flat_sets[k];

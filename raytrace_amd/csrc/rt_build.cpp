@@ -848,7 +848,12 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     // kLeaf): bunny-Cornell 144.0 -> 139.7 ms binary64, demo1 63.9 -> 61.6 (profiles/r3/agg)
     S.leaf_kind = n == (int)prefix.size() ? 0 : static_tris ? 1 : static_spheres ? 2 : 0;
     S.leaf_exit_pct = spheres_only ? 100 : sc->n_media > 0 ? 55 : 25;
-    if (const char* e = std::getenv("RT_AMD_LEAF_EXIT_PCT")) S.leaf_exit_pct = std::max(1, std::min(100, atoi(e)));
+    // the binary64 media kernel (3 waves/SIMD, its whole pawn BVH staged in LDS) tests leaves
+    // later: pawn+fog 544.8 -> 538.7 ms at 70 % (80: 547, 40: 560); its FP32 kernel keeps 55
+    // (70: +3.6 %)
+    S.leaf_exit_pct64 = !spheres_only && sc->n_media > 0 ? 70 : S.leaf_exit_pct;
+    if (const char* e = std::getenv("RT_AMD_LEAF_EXIT_PCT"))
+      S.leaf_exit_pct = S.leaf_exit_pct64 = std::max(1, std::min(100, atoi(e)));
     // and the decoupled lane loop's exit (KernelParams::trav_exit_pct): pawn+fog 386 -> 376 ms at
     // 75 %, demo1 49.2 -> 48.5 at 25 %, the bunny flat between 50 and 75
     S.trav_exit_pct = spheres_only ? 25 : sc->n_media > 0 ? 75 : 50;

@@ -339,6 +339,7 @@ struct HostScene {
   bool noise = false;  // some texture is a noise / marble texture
   bool uv_tex = false;     // some material reads a non-constant texture (RT_VAR_TEX)
   int leaf_exit_pct = 100;  // BVH traversal policy for this scene (KernelParams::leaf_exit_pct)
+  int leaf_exit_pct64 = 100;  // ... for the binary64 kernels
   int trav_exit_pct = 50;   // and its lane-loop exit (KernelParams::trav_exit_pct)
   bool full_mats = false;  // some material is not lightSource / pitchBlack / lambertian (RT_VAR_MATS)
   int n_instances = 0;     // two-level instancing (RT_VAR_INST)

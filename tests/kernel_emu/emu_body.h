@@ -103,7 +103,7 @@ int render(const HostScene& H, const rt_camera_settings* cs, uint64_t seed, cons
   P.instances = A.instances.data();
   P.out = out;
   P.surface_root = H.surface_root;
-  P.leaf_exit_pct = H.leaf_exit_pct;
+  P.leaf_exit_pct = RT_F64 ? H.leaf_exit_pct64 : H.leaf_exit_pct;
   P.surface_prefix = H.flat ? 0 : 1;
   P.n_media = H.n_media;
   for (int k = 0; k < H.n_media; ++k) P.media[k] = A.media[k];
