@@ -190,6 +190,38 @@ def roofline_of(config, precision, kernel_ms, launch_ms, share, samples_per_laun
     return r
 
 
+def abi_device_list(world, cs, seed, devices, precision, frames, warmup=2):
+    """The drop-in's own multi-GPU path: ONE process rendering the whole frame through the C ABI's
+    device list (rt_multi_scene_create / rt_multi_render: shard k on devices[k], peer-copy gather
+    into devices[0], one device-to-host copy), as the Haskell binding calls it (Device.hs passes
+    every visible device; the reference's `-threaded -N` analogue, Ray.hs:238).  Host-buffer
+    output, so the time includes the device-to-host copy of the frame."""
+    import hashlib
+    import numpy as np
+    from raytrace_amd.ray import MultiDeviceScene
+    m = MultiDeviceScene(world, devices)
+    try:
+        for _ in range(warmup):  # uploads, occupancy queries, the resident buffers
+            m.render(cs, seed, precision=precision, row_block=1)
+        kms, allocs = [], 0
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            st = {}
+            img = m.render(cs, seed, precision=precision, row_block=1, stats=st)
+            kms.append(st["kernel_ms"])
+            allocs += st["device_allocs"]
+        dt = time.perf_counter() - t0
+    finally:
+        m.close()
+    samples = img.shape[0] * img.shape[1] * cs.cs_samplesPerPixel
+    return {"devices": list(devices), "dtype": precision, "frames": frames,
+            "ms_per_frame": round(dt / frames * 1e3, 4), "value": round(samples * frames / dt / 1e6, 2),
+            "unit": "Msamples/s", "kernel_ms_max_device": round(sum(kms) / len(kms), 4),
+            "device_allocs_timed": allocs,
+            "sha16": hashlib.sha256(np.ascontiguousarray(img).tobytes()).hexdigest()[:16],
+            "note": "one process, rt_multi_render over the device list (C-ABI drop-in path), host-buffer output"}
+
+
 def spawn_ranks(n):
     """`bench.py --gpus N` without a launcher: run this same command as N ranks under
     torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) and return its exit code.
@@ -237,6 +269,8 @@ def main():
                          "many seconds (the per-frame time settles after a few hundred ms); 0: exactly W")
     ap.add_argument("--sim-shards", type=int, default=1,
                     help="diagnostic, one process: render only shard 0 of N (one rank's share of an N-GPU frame)")
+    ap.add_argument("--no-abi-devices", action="store_true",
+                    help="skip the abi_device_list record (rank 0, after the ranks' measurement)")
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="nccl (= RCCL, the real path); gloo gathers through host memory (N>1 rehearsal on one "
                          "GPU, with RT_BENCH_ONE_DEVICE=1 mapping every rank to device 0); auto: gloo with "
@@ -446,11 +480,23 @@ def main():
             _, f32 = record("f32")
             f32["note"] = "FP32 fast path (rt_exec.flags RT_EXEC_F32), same frames, measured after the f64 line"
             line["f32_fast_path"] = f32
-        print(json.dumps(line), flush=True)
     if n > 1:
         dist.barrier()
         dist.destroy_process_group()
     scene.close()
+    if rank == 0:
+        # the drop-in's own multi-GPU path over the same N GPUs, after the ranks' measurement (the
+        # process group is gone): rank 0 alone drives every device through the C-ABI device list
+        if not args.no_abi_devices and n_sh == n:
+            devs = [0] * n if one_device else list(range(n))
+            try:
+                line["abi_device_list"] = abi_device_list(world, cs, seed, devs, precisions[0],
+                                                          frames=max(args.steps, 5))
+                line["abi_device_list"]["sha16_equals_line"] = (
+                    main_rec["check"] is not None and line["abi_device_list"]["sha16"] == main_rec["check"]["sha16"])
+            except Exception as e:  # never break the bench line
+                line["abi_device_list"] = {"error": repr(e)}
+        print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

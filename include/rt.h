@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 /* status codes */
 #define RT_OK 0
@@ -188,7 +188,7 @@ typedef struct rt_camera_settings {
   const rt_redirect_target* redirect_targets;
 } rt_camera_settings;
 
-/* rt_exec.flags */
+/* rt_exec.flags (any other bit, or both RT_EXEC_ENCODE8_* bits, is RT_E_INVALID) */
 #define RT_EXEC_F32 1          /* FP32 kernel, float output (default: binary64, double output) */
 /* 8-bit output (rt_render / rt_multi_render only): out_rgb receives uint8 codes, one per channel,
    exactly what writeImage (sRGB) / writeImageSqrt (sqrt) store (Ray.hs:248-260):
@@ -233,6 +233,10 @@ typedef struct rt_stats {
   int64_t samples;      /* pixels x spp rendered by this call */
   int32_t bvh_nodes;    /* nodes of all sets */
   int32_t max_stack;    /* deepest traversal stack the build can require */
+  int32_t device_allocs; /* device allocations (hipMalloc) this call made: a resident multi-device
+                            scene allocates its buffers on its first render (or a larger frame)
+                            only, so later rt_multi_render calls report 0 (ABI v5) */
+  int32_t pad;
 } rt_stats;
 
 typedef struct rt_device_scene rt_device_scene;   /* opaque, device-resident scene */
@@ -260,7 +264,11 @@ int rt_render(const rt_camera_settings* cs, const rt_scene* scene, uint64_t seed
 
 /* Device-resident path (used when inputs already live in HBM, e.g. bench.py / torch callers).
  * The scene is built on the host at create; a precision's records are uploaded on its first
- * render (rt_stats.upload_ms of rt_scene_stats covers what has been uploaded so far). */
+ * render (rt_stats.upload_ms of rt_scene_stats covers what has been uploaded so far).  That first
+ * render of a precision is therefore NOT asynchronous: it makes synchronous device allocations and
+ * copies (and queries the kernel's occupancy) before it enqueues; a caller that captures the
+ * stream into a HIP graph, or needs the first call to return at once, renders that precision
+ * once beforehand. */
 int rt_scene_create(const rt_scene* scene, int32_t device, rt_device_scene** out);
 int rt_scene_destroy(rt_device_scene* s);
 int rt_scene_stats(const rt_device_scene* s, rt_stats* stats);
@@ -273,7 +281,10 @@ int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint
 
 /* Multi-device resident scene (one process, many GPUs; what a caller that renders the same scene
  * more than once keeps between rt_render-like calls): one host build, concurrent uploads to the
- * distinct devices of the list.  rt_multi_render renders as rt_render does with this device list
+ * distinct devices of the list, and per device its tile, render workspace, stream and events plus
+ * the first device's gather and 8-bit buffers, all kept across renders (allocated on the first
+ * render, or again for a larger frame: rt_stats.device_allocs).  Renders of one scene are
+ * serialised (a mutex); the status word (traversal-stack overflow) is cleared before each.  rt_multi_render renders as rt_render does with this device list
  * (ex->n_devices must be 0; ex->n_shards 1, row_block and flags as in rt_render) into the
  * caller's host buffer out_rgb (h * width * 3 doubles, floats with RT_EXEC_F32, bytes with
  * RT_EXEC_ENCODE8_*).  A list of one device also renders an rt_exec shard (n_shards > 1). */

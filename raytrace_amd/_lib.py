@@ -10,7 +10,10 @@ import numpy as np
 from .errors import RtDeviceError, RtError, RtInvalid, RtUnsupported
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("RT_AMD_LIB") or os.path.join(HERE, "_lib", "librt_amd.so")  # env: experiment builds
+# RT_AMD_LIB (an experiment build of the library) is honoured only with RT_AMD_EXPERIMENTS set, like
+# the library's own RT_AMD_* knobs (rt_internal.h rt_knob)
+_EXPERIMENTS = os.environ.get("RT_AMD_EXPERIMENTS", "0") not in ("", "0")
+LIB_PATH = (_EXPERIMENTS and os.environ.get("RT_AMD_LIB")) or os.path.join(HERE, "_lib", "librt_amd.so")
 
 RT_OK, RT_E_GENERIC, RT_E_INVALID, RT_E_UNSUPPORTED, RT_E_HIP, RT_E_STACK = 0, -1, -2, -3, -4, -5
 
@@ -55,7 +58,7 @@ RT_EXEC_F32 = 1  # rt_exec.flags: FP32 kernel, float output (default: binary64, 
 RT_EXEC_ENCODE8_SRGB = 2  # rt_render output: uint8 codes of writeImage (sRGB)
 RT_EXEC_ENCODE8_SQRT = 4  # rt_render output: uint8 codes of writeImageSqrt
 ENCODINGS = {None: 0, "srgb": RT_EXEC_ENCODE8_SRGB, "sqrt": RT_EXEC_ENCODE8_SQRT}
-ABI_VERSION = 4
+ABI_VERSION = 5
 PRECISIONS = {"f64": np.float64, "f32": np.float32}
 
 
@@ -67,7 +70,8 @@ class RtExec(ctypes.Structure):
 
 class RtStats(ctypes.Structure):
     _fields_ = [("upload_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
-                ("samples", ctypes.c_int64), ("bvh_nodes", ctypes.c_int32), ("max_stack", ctypes.c_int32)]
+                ("samples", ctypes.c_int64), ("bvh_nodes", ctypes.c_int32), ("max_stack", ctypes.c_int32),
+                ("device_allocs", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
 _lib = None

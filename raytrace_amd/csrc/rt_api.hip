@@ -126,11 +126,30 @@ bool& rt_device_scene::have<float>() const { return have_f32; }
 template <>
 bool& rt_device_scene::have<double>() const { return have_f64; }
 
+// The resident per-shard buffers of a multi-device scene: shard k's tile, its render workspace
+// (fixed-point sums, NaN flags, queue heads), its stream and timing events on devices[k]
+struct MultiPart {
+  int device = 0;
+  void* d_tile = nullptr;
+  size_t tile_cap = 0;
+  char* ws = nullptr;
+  size_t ws_cap = 0;
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+};
 struct rt_multi_scene {
   std::vector<int> devices;                // shard k renders on devices[k]
   std::vector<rt_device_scene*> scenes;    // one per DISTINCT device, in first-use order
   std::vector<int> scene_of;               // devices[k] -> scenes index
   double build_ms = 0, upload_ms = 0;      // one host build; the uploads' wall time (concurrent)
+  // kept across renders (grown when a frame needs more): no allocation after the first render
+  std::mutex mu;                           // one render at a time: the buffers below are shared
+  std::vector<MultiPart> parts;            // per devices[k]
+  void* d_gather = nullptr;                // first device: the n tiles in global row order
+  size_t gather_cap = 0;
+  uint8_t* d_codes = nullptr;              // first device: the 8-bit epilogue's output
+  size_t codes_cap = 0;
+  hipStream_t st0 = nullptr;               // first device: epilogue and device-to-host copy
 };
 
 namespace {
@@ -164,7 +183,7 @@ int ensure_precision(const rt_device_scene* s) {
     const int used = rt_render_acc_lds((const KernelParamsT<R>*)nullptr, s->variant) +
                      (s->stack_depth + 1) * block * (int)sizeof(int);
     A.lds_nodes = std::max(0, std::min(s->host->surface_nodes, (budget - used) / 64));
-    if (const char* e = std::getenv("RT_AMD_LDS_NODES")) A.lds_nodes = std::min(A.lds_nodes, std::max(0, atoi(e)));
+    if (const char* e = rt_knob("RT_AMD_LDS_NODES")) A.lds_nodes = std::min(A.lds_nodes, std::max(0, atoi(e)));
   }
   A.resident_blocks = rt_render_resident_blocks((const KernelParamsT<R>*)nullptr, s->device, s->stack_depth,
                                                 s->variant, A.lds_nodes);
@@ -178,9 +197,20 @@ int ensure_precision(const rt_device_scene* s) {
   return RT_OK;
 }
 
+// the stream-ordered workspace of one render: fixed-point sums, NaN flags, queue head words
+size_t workspace_bytes(size_t tile_pixels, int acc_words, size_t* off_flag, size_t* off_ctr) {
+  const size_t of = tile_pixels * acc_words * sizeof(long long);
+  const size_t oc = of + ((tile_pixels * sizeof(unsigned) + 255) & ~(size_t)255);
+  if (off_flag) *off_flag = of;
+  if (off_ctr) *off_ctr = oc;
+  return oc + 256 * 8;  // up to 8 queue head words (rt_render_kernel.h RT_QUEUES)
+}
+
+// ws / ws_cap: a caller-held workspace (a multi-device scene's resident one), or null: the render
+// takes one from the stream-ordered pool (hipMallocAsync / hipFreeAsync)
 template <class R>
 int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex, R* d_out,
-                 void* hip_stream) {
+                 void* hip_stream, char* ws_given = nullptr, size_t ws_cap = 0) {
   if (int rc = ensure_precision<R>(s)) return rc;
   const DevArrays<R>& A = s->arrays<R>();
   KernelParamsT<R> P;
@@ -219,12 +249,12 @@ int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_
   HIP_TRY(hipSetDevice(s->device));
   // stream-ordered workspace: fixed-point sums, NaN flags, queue counter (graph-capturable)
   const size_t tile_pixels = (size_t)P.tile_rows * P.cam.width;
-  const size_t off_flag = tile_pixels * RT_ACC_WORDS(R) * sizeof(long long);
-  const size_t off_ctr = off_flag + ((tile_pixels * sizeof(unsigned) + 255) & ~(size_t)255);
-  const size_t bytes = off_ctr + 256 * 8;  // up to 8 queue head words (rt_render_kernel.h RT_QUEUES)
+  size_t off_flag = 0, off_ctr = 0;
+  const size_t bytes = workspace_bytes(tile_pixels, RT_ACC_WORDS(R), &off_flag, &off_ctr);
   hipStream_t st = (hipStream_t)hip_stream;
-  char* ws = nullptr;
-  HIP_TRY(hipMallocAsync((void**)&ws, bytes, st));
+  char* ws = ws_given && ws_cap >= bytes ? ws_given : nullptr;
+  const bool own = ws == nullptr;
+  if (own) HIP_TRY(hipMallocAsync((void**)&ws, bytes, st));
   HIP_TRY(hipMemsetAsync(ws, 0, bytes, st));
   P.accum = (unsigned long long*)ws;
   P.nanflag = (unsigned int*)(ws + off_flag);
@@ -235,14 +265,23 @@ int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_
   // (profiles/r3/iso): with 8 free slots the FP32 resolve still takes 3.1 ms, starved by the next
   // frame's grid; binary64's runs in 23 us either way (its kernel leaves VGPRs free) — so 0.
   int reserve = A.resident_blocks > 16 * RT_GRID_RESERVE ? RT_GRID_RESERVE : 0;
-  if (const char* e = std::getenv("RT_AMD_GRID_RESERVE")) reserve = std::max(0, std::min(A.resident_blocks - 1, atoi(e)));
+  if (const char* e = rt_knob("RT_AMD_GRID_RESERVE")) reserve = std::max(0, std::min(A.resident_blocks - 1, atoi(e)));
   if (rt_launch_render(P, A.resident_blocks - reserve, s->variant, hip_stream) || rt_launch_resolve(P, hip_stream))
     rc = fail(RT_E_HIP, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
-  HIP_TRY(hipFreeAsync(ws, st));
+  if (own) HIP_TRY(hipFreeAsync(ws, st));
   return rc;
 }
 
 bool exec_f32(const rt_exec* ex) { return ex && (ex->flags & RT_EXEC_F32) != 0; }
+
+// rt_exec.flags: known bits only, at most one 8-bit encoding
+int check_flags(const rt_exec* ex) {
+  const int known = RT_EXEC_F32 | RT_EXEC_ENCODE8_SRGB | RT_EXEC_ENCODE8_SQRT;
+  if (ex->flags & ~known) return fail(RT_E_INVALID, "unknown rt_exec.flags bits 0x%x", ex->flags & ~known);
+  if ((ex->flags & RT_EXEC_ENCODE8_SRGB) && (ex->flags & RT_EXEC_ENCODE8_SQRT))
+    return fail(RT_E_INVALID, "rt_exec.flags: RT_EXEC_ENCODE8_SRGB and RT_EXEC_ENCODE8_SQRT are exclusive");
+  return RT_OK;
+}
 
 // rt_exec.flags -> the 8-bit epilogue's encoding (0 sRGB, 1 sqrt) or -1 (linear output)
 int exec_encoding(const rt_exec* ex) {
@@ -317,6 +356,8 @@ int check_device(int device) {
   return RT_OK;
 }
 
+void multi_destroy(rt_multi_scene* M);
+
 // A multi-device scene from one host build: the distinct devices upload CONCURRENTLY (one host
 // thread each; the host build is shared, never repeated per device).  prec_mask: precisions to
 // upload now (the rest on first render).
@@ -356,6 +397,21 @@ int multi_create(const std::shared_ptr<const HostScene>& H, const int32_t* devic
       delete M;
       return fail(rcs[j], "device %d: %s", distinct[j], errs[j].c_str());
     }
+  // per shard: its stream and timing events (its tile and workspace come with the first render)
+  M->parts.resize(n);
+  for (int k = 0; k < n; ++k) {
+    MultiPart& q = M->parts[k];
+    q.device = devices[k];
+    if (hipSetDevice(q.device) != hipSuccess || hipStreamCreateWithFlags(&q.st, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&q.e0) != hipSuccess || hipEventCreate(&q.e1) != hipSuccess) {
+      multi_destroy(M);
+      return fail(RT_E_HIP, "stream / events on device %d", devices[k]);
+    }
+  }
+  if (hipSetDevice(devices[0]) != hipSuccess || hipStreamCreateWithFlags(&M->st0, hipStreamNonBlocking) != hipSuccess) {
+    multi_destroy(M);
+    return fail(RT_E_HIP, "stream on device %d", devices[0]);
+  }
   // the first device gathers the shard tiles: let every other device write into its memory
   // over xGMI (peer access; without it HIP stages the copies itself)
   for (size_t j = 1; j < distinct.size(); ++j) {
@@ -372,15 +428,44 @@ int multi_create(const std::shared_ptr<const HostScene>& H, const int32_t* devic
 
 void multi_destroy(rt_multi_scene* M) {
   if (!M) return;
+  for (MultiPart& q : M->parts) {
+    (void)hipSetDevice(q.device);
+    if (q.st) (void)hipStreamSynchronize(q.st);
+    if (q.e0) (void)hipEventDestroy(q.e0);
+    if (q.e1) (void)hipEventDestroy(q.e1);
+    if (q.st) (void)hipStreamDestroy(q.st);
+    (void)hipFree(q.d_tile);
+    (void)hipFree(q.ws);
+  }
+  if (!M->devices.empty()) {
+    (void)hipSetDevice(M->devices[0]);
+    if (M->st0) (void)hipStreamDestroy(M->st0);
+    (void)hipFree(M->d_gather);
+    (void)hipFree(M->d_codes);
+  }
   for (rt_device_scene* s : M->scenes) destroy_scene(s);
   delete M;
 }
 
+// grow a resident device buffer to `need` bytes (on the current device); counts the allocation
+int grow(void** p, size_t* cap, size_t need, int* allocs) {
+  if (*cap >= need && *p) return RT_OK;
+  (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  HIP_TRY(hipMalloc(p, need ? need : 16));
+  *cap = need;
+  ++*allocs;
+  return RT_OK;
+}
+
 // Render the image (device list: shard k of n on devices[k]) or, with one device, the rt_exec
 // shard; gather on the first device; optional 8-bit epilogue there; ONE copy to the host buffer.
-int multi_render(const rt_multi_scene* M, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex,
+// Every buffer, stream and event is the scene's own (rt_multi_scene), kept across renders.
+int multi_render(rt_multi_scene* M, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex,
                  void* out_host, rt_stats* stats, double build_ms) {
   auto t0 = std::chrono::steady_clock::now();
+  if (int rc = check_flags(ex)) return rc;
   const int h = rt_host_image_height(cs);
   if (h <= 0 || cs->image_width <= 0) return fail(RT_E_INVALID, "image %dx%d must be non-empty", cs->image_width, h);
   const int n = (int)M->devices.size();
@@ -393,24 +478,23 @@ int multi_render(const rt_multi_scene* M, const rt_camera_settings* cs, uint64_t
     int rc = rt_host_make_params(cs, seed, ex, P, err);
     if (rc) return fail(rc, "%s", err.c_str());
   }
+  std::lock_guard<std::mutex> lock(M->mu);
   const bool f32 = exec_f32(ex);
   const int encoding = exec_encoding(ex);
   const size_t esize = f32 ? sizeof(float) : sizeof(double);
   const size_t row_bytes = (size_t)cs->image_width * 3 * esize;
-  struct Part {
+  struct Job {
     rt_exec ex{};
     int rows = 0;
-    void* d_tile = nullptr;
-    hipStream_t st = nullptr;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
     float ms = 0;
     int rc = RT_OK;
     std::string err;
     double prep_ms = 0;
+    int allocs = 0;
   };
-  std::vector<Part> parts(n);
+  std::vector<Job> jobs(n);
   for (int k = 0; k < n; ++k) {
-    Part& p = parts[k];
+    Job& p = jobs[k];
     p.ex = *ex;
     p.ex.n_devices = 0;
     p.ex.devices = nullptr;
@@ -426,45 +510,51 @@ int multi_render(const rt_multi_scene* M, const rt_camera_settings* cs, uint64_t
   // tiles), or the single shard's tile itself
   const int dev0 = M->devices[0];
   const int rb = ex->row_block;
-  const size_t gather_rows = n > 1 ? (size_t)n * parts[0].rows : (size_t)rows_out;
-  void* d_gather = nullptr;
-  uint8_t* d_codes = nullptr;
-  hipStream_t st0 = nullptr;
+  const size_t gather_rows = n > 1 ? (size_t)n * jobs[0].rows : (size_t)rows_out;
+  int allocs = 0;
   int rc = RT_OK;
-  if (hipSetDevice(dev0) != hipSuccess || hipStreamCreateWithFlags(&st0, hipStreamNonBlocking) != hipSuccess)
-    rc = fail(RT_E_HIP, "stream on device %d", dev0);
-  if (!rc && n > 1 && hipMalloc(&d_gather, gather_rows * row_bytes) != hipSuccess)
-    rc = fail(RT_E_HIP, "hipMalloc(gather %zu bytes) failed", gather_rows * row_bytes);
-  if (!rc && encoding >= 0 && hipMalloc((void**)&d_codes, std::max<size_t>(16, gather_rows * cs->image_width * 3)) != hipSuccess)
-    rc = fail(RT_E_HIP, "hipMalloc(codes) failed");
+  if (hipSetDevice(dev0) != hipSuccess) rc = fail(RT_E_HIP, "device %d", dev0);
+  if (!rc && n > 1) rc = grow(&M->d_gather, &M->gather_cap, gather_rows * row_bytes, &allocs);
+  if (!rc && encoding >= 0)
+    rc = grow((void**)&M->d_codes, &M->codes_cap, std::max<size_t>(16, gather_rows * cs->image_width * 3), &allocs);
+  // a stack overflow of an earlier render must not fail this one: clear each device's status word
+  for (size_t j = 0; j < M->scenes.size() && !rc; ++j) {
+    const rt_device_scene* s = M->scenes[j];
+    const MultiPart& q = M->parts[std::find(M->scene_of.begin(), M->scene_of.end(), (int)j) - M->scene_of.begin()];
+    if (hipSetDevice(s->device) != hipSuccess || hipMemsetAsync(s->status, 0, 4 * sizeof(int), q.st) != hipSuccess ||
+        hipStreamSynchronize(q.st) != hipSuccess)
+      rc = fail(RT_E_HIP, "status reset on device %d", s->device);
+  }
   if (!rc) {
     std::vector<std::thread> th;
     for (int k = 0; k < n; ++k)
       th.emplace_back([&, k] {
-        Part& p = parts[k];
+        Job& p = jobs[k];
+        MultiPart& q = M->parts[k];
         const rt_device_scene* s = M->scenes[M->scene_of[k]];
         auto run = [&]() -> int {
           HIP_TRY(hipSetDevice(s->device));
           auto tp = std::chrono::steady_clock::now();
           if (int r = ensure_precisions(s, f32 ? 1 : 2)) return r;
           p.prep_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp).count();
-          const size_t bytes = (size_t)p.rows * row_bytes;
-          HIP_TRY(hipMalloc(&p.d_tile, bytes ? bytes : 16));
-          HIP_TRY(hipStreamCreateWithFlags(&p.st, hipStreamNonBlocking));
-          HIP_TRY(hipEventCreate(&p.e0));
-          HIP_TRY(hipEventCreate(&p.e1));
-          HIP_TRY(hipEventRecord(p.e0, p.st));
-          if (int r = rt_render_async(s, cs, seed, &p.ex, p.d_tile, p.st)) return r;
-          HIP_TRY(hipEventRecord(p.e1, p.st));
+          const size_t tile_pixels = (size_t)p.rows * cs->image_width;
+          if (int r = grow(&q.d_tile, &q.tile_cap, tile_pixels * 3 * esize, &p.allocs)) return r;
+          const size_t wsb = workspace_bytes(tile_pixels, f32 ? RT_ACC_WORDS(float) : RT_ACC_WORDS(double), nullptr, nullptr);
+          if (int r = grow((void**)&q.ws, &q.ws_cap, wsb, &p.allocs)) return r;
+          HIP_TRY(hipEventRecord(q.e0, q.st));
+          const int r = f32 ? render_async<float>(s, cs, seed, &p.ex, (float*)q.d_tile, q.st, q.ws, q.ws_cap)
+                            : render_async<double>(s, cs, seed, &p.ex, (double*)q.d_tile, q.st, q.ws, q.ws_cap);
+          if (r) return r;
+          HIP_TRY(hipEventRecord(q.e1, q.st));
           if (n > 1) {
             // shard-local row block b is global block b n + k: one strided copy into the first
             // device's framebuffer (peer-to-peer over xGMI for another device)
             const size_t w = (size_t)rb * row_bytes;
-            HIP_TRY(hipMemcpy2DAsync((char*)d_gather + (size_t)k * w, (size_t)n * w, p.d_tile, w, w,
-                                     (size_t)p.rows / rb, hipMemcpyDeviceToDevice, p.st));
+            HIP_TRY(hipMemcpy2DAsync((char*)M->d_gather + (size_t)k * w, (size_t)n * w, q.d_tile, w, w,
+                                     (size_t)p.rows / rb, hipMemcpyDeviceToDevice, q.st));
           }
-          HIP_TRY(hipStreamSynchronize(p.st));
-          HIP_TRY(hipEventElapsedTime(&p.ms, p.e0, p.e1));
+          HIP_TRY(hipStreamSynchronize(q.st));
+          HIP_TRY(hipEventElapsedTime(&p.ms, q.e0, q.e1));
           return RT_OK;
         };
         p.rc = run();
@@ -472,8 +562,9 @@ int multi_render(const rt_multi_scene* M, const rt_camera_settings* cs, uint64_t
       });
     for (auto& t : th) t.join();
     for (int k = 0; k < n && !rc; ++k)
-      if (parts[k].rc) rc = fail(parts[k].rc, "device %d: %s", M->devices[k], parts[k].err.c_str());
+      if (jobs[k].rc) rc = fail(jobs[k].rc, "device %d: %s", M->devices[k], jobs[k].err.c_str());
   }
+  for (const Job& p : jobs) allocs += p.allocs;
   int status = 0;
   for (size_t j = 0; j < M->scenes.size() && !rc; ++j) {
     int ps = 0;
@@ -482,7 +573,7 @@ int multi_render(const rt_multi_scene* M, const rt_camera_settings* cs, uint64_t
     status |= ps;
   }
   if (!rc && status) rc = fail(RT_E_STACK, "BVH traversal stack overflow");
-  const void* d_img = n > 1 ? d_gather : parts[0].d_tile;
+  const void* d_img = n > 1 ? M->d_gather : M->parts[0].d_tile;
   const size_t out_rows = n > 1 ? (size_t)h : (size_t)rows_out;
   if (!rc) {
     (void)hipSetDevice(dev0);
@@ -490,20 +581,20 @@ int multi_render(const rt_multi_scene* M, const rt_camera_settings* cs, uint64_t
     size_t bytes = out_rows * row_bytes;
     if (encoding >= 0) {
       const int64_t nv = (int64_t)out_rows * cs->image_width * 3;
-      if (rt_launch_encode8(d_img, f32 ? 0 : 1, d_codes, nv, encode8_table(encoding), encoding, st0))
+      if (rt_launch_encode8(d_img, f32 ? 0 : 1, M->d_codes, nv, encode8_table(encoding), encoding, M->st0))
         rc = fail(RT_E_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
-      src = d_codes;
+      src = M->d_codes;
       bytes = (size_t)nv;
     }
-    if (!rc && (hipMemcpyAsync(out_host, src, bytes, hipMemcpyDeviceToHost, st0) != hipSuccess ||
-                hipStreamSynchronize(st0) != hipSuccess))
+    if (!rc && (hipMemcpyAsync(out_host, src, bytes, hipMemcpyDeviceToHost, M->st0) != hipSuccess ||
+                hipStreamSynchronize(M->st0) != hipSuccess))
       rc = fail(RT_E_HIP, "copy back: %s", hipGetErrorString(hipGetLastError()));
   }
   if (stats && !rc) {
     std::memset(stats, 0, sizeof *stats);
     double prep = 0;
     float ms = 0;
-    for (const Part& p : parts) {
+    for (const Job& p : jobs) {
       prep = std::max(prep, p.prep_ms);
       ms = std::max(ms, p.ms);
     }
@@ -512,21 +603,9 @@ int multi_render(const rt_multi_scene* M, const rt_camera_settings* cs, uint64_t
     stats->samples = (int64_t)rows_out * cs->image_width * cs->samples_per_pixel;
     stats->bvh_nodes = M->scenes[0]->n_nodes;
     stats->max_stack = M->scenes[0]->max_depth;
+    stats->device_allocs = allocs;
     stats->total_ms = build_ms + std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
-  for (int k = 0; k < n; ++k) {
-    Part& p = parts[k];
-    (void)hipSetDevice(M->devices[k]);
-    if (p.st) (void)hipStreamSynchronize(p.st);
-    if (p.e0) (void)hipEventDestroy(p.e0);
-    if (p.e1) (void)hipEventDestroy(p.e1);
-    if (p.st) (void)hipStreamDestroy(p.st);
-    (void)hipFree(p.d_tile);
-  }
-  (void)hipSetDevice(dev0);
-  if (st0) (void)hipStreamDestroy(st0);
-  (void)hipFree(d_gather);
-  (void)hipFree(d_codes);
   return rc;
 }
 
@@ -604,6 +683,7 @@ int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint
                     void* d_out_rgb, void* hip_stream) {
   if (!s || !d_out_rgb || !ex || !cs) return fail(RT_E_INVALID, "null argument");
   if (ex->n_devices != 0) return fail(RT_E_INVALID, "rt_render_async renders on the scene's device (n_devices = 0)");
+  if (int rc = check_flags(ex)) return rc;
   if (exec_encoding(ex) >= 0) return fail(RT_E_INVALID, "rt_render_async writes linear RGB (use rt_encode8_async)");
   if (exec_f32(ex)) return render_async<float>(s, cs, seed, ex, (float*)d_out_rgb, hip_stream);
   return render_async<double>(s, cs, seed, ex, (double*)d_out_rgb, hip_stream);
@@ -629,7 +709,8 @@ int rt_multi_render(const rt_multi_scene* m, const rt_camera_settings* cs, uint6
                     void* out, rt_stats* stats) {
   if (!m || !cs || !ex || !out) return fail(RT_E_INVALID, "null argument");
   if (ex->n_devices != 0) return fail(RT_E_INVALID, "rt_multi_render renders on the scene's devices (n_devices = 0)");
-  const int rc = multi_render(m, cs, seed, ex, out, stats, 0.0);
+  // the scene's resident buffers are its internal state (the caller's handle stays const)
+  const int rc = multi_render(const_cast<rt_multi_scene*>(m), cs, seed, ex, out, stats, 0.0);
   if (!rc && stats) stats->upload_ms += m->build_ms;  // the scene's one-time cost, as rt_render reports it
   return rc;
 }
@@ -640,6 +721,7 @@ int rt_render(const rt_camera_settings* cs, const rt_scene* scene, uint64_t seed
   int h = rt_host_image_height(cs);
   if (h <= 0 || cs->image_width <= 0) return fail(RT_E_INVALID, "image %dx%d must be non-empty", cs->image_width, h);
   if (rt_host_shard_rows(h, ex) < 0) return fail(RT_E_INVALID, "invalid rt_exec");
+  if (int rc = check_flags(ex)) return rc;
   if (ex->n_devices < 0 || ex->n_devices > RT_MAX_DEVICES || (ex->n_devices > 0 && !ex->devices))
     return fail(RT_E_INVALID, "invalid device list (%d devices)", ex->n_devices);
   if (ex->n_devices > 0 && ex->n_shards != 1)

@@ -18,6 +18,12 @@
 #include "rt_encode8_table.h"
 #include "rt_internal.h"
 
+const char* rt_knob(const char* name) {
+  const char* on = std::getenv("RT_AMD_EXPERIMENTS");
+  if (!on || !*on || std::atoi(on) == 0) return nullptr;
+  return std::getenv(name);
+}
+
 namespace {
 
 struct d3 {
@@ -515,7 +521,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
       alias[k] = eq ? 1 : 0;
     }
   }
-  if (const char* e = std::getenv("RT_AMD_NO_ALIAS"))  // experiments: always traverse boundaries
+  if (const char* e = rt_knob("RT_AMD_NO_ALIAS"))  // experiments: always traverse boundaries
     if (atoi(e)) std::fill(alias.begin(), alias.end(), 0);
   if (sc->n_instances > 0) std::fill(alias.begin(), alias.end(), 0);  // the surface set also holds placements
 
@@ -530,7 +536,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   int prefix_cnt[3] = {0, 0, 0};
   {
     bool want = (int)sets[0].size() > RT_FLAT_MAX + RT_PREFIX_MAX;
-    if (const char* e = std::getenv("RT_AMD_NO_PREFIX"))  // experiments: everything in the BVH
+    if (const char* e = rt_knob("RT_AMD_NO_PREFIX"))  // experiments: everything in the BVH
       if (atoi(e)) want = false;
     if (want) {
       auto area = [](const double* lo, const double* hi) {
@@ -546,7 +552,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
         }
       const double root_area = area(lo, hi);
       double frac = RT_PREFIX_AREA;
-      if (const char* e = std::getenv("RT_AMD_PREFIX_AREA")) frac = atof(e);  // experiments
+      if (const char* e = rt_knob("RT_AMD_PREFIX_AREA")) frac = atof(e);  // experiments
       std::vector<std::pair<double, int>> big;  // (area, position in sets[0])
       for (size_t j = 0; j < sets[0].size(); ++j) {
         const BuildPrim& b = sets[0][j];
@@ -560,7 +566,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
       // then outliers: a primitive that alone holds a face of the remaining set's box out by a
       // lot (the Cornell light above the bunny: without it the BVH root shrinks to the bunny)
       double shrink = RT_PREFIX_SHRINK;
-      if (const char* e = std::getenv("RT_AMD_PREFIX_SHRINK")) shrink = atof(e);  // experiments
+      if (const char* e = rt_knob("RT_AMD_PREFIX_SHRINK")) shrink = atof(e);  // experiments
       for (int added = (int)big.size(); added < RT_PREFIX_MAX && shrink < 1.0; ++added) {
         auto bounds_without = [&](int skip, double* l, double* h) {
           for (int a = 0; a < 3; ++a) {
@@ -627,7 +633,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     bool spheres = true;
     for (const BuildPrim& b : sets[s]) spheres = spheres && b.inst < 0 && sc->prims[b.index].kind == RT_PRIM_SPHERE;
     int leaf_max = spheres ? RT_LEAF_MAX : 2;
-    if (const char* e = std::getenv("RT_AMD_LEAF_MAX")) leaf_max = std::max(1, std::min(RT_FLAT_MAX, atoi(e)));
+    if (const char* e = rt_knob("RT_AMD_LEAF_MAX")) leaf_max = std::max(1, std::min(RT_FLAT_MAX, atoi(e)));
     rt_build_bvh(sets[s], (int)(S.nodes.size() / 16), (int)order.size(), bo, leaf_max);
     S.nodes.insert(S.nodes.end(), bo.nodes.begin(), bo.nodes.end());
     order.insert(order.end(), bo.order.begin(), bo.order.end());
@@ -652,6 +658,9 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     blas_depth = std::max(blas_depth, bo.max_depth);
   }
   if (sc->n_instances > 0) S.max_depth = std::max(S.max_depth, surface_depth + 1 + blas_depth + 1);
+  if (S.nodes.size() / 16 >= (size_t)RT_MAX_NODES)
+    return fail(err, RT_E_UNSUPPORTED, "%zu BVH nodes exceed the kernels' 32-bit node offsets (%d)", S.nodes.size() / 16,
+                RT_MAX_NODES);
   if (S.max_depth > RT_STACK_DEPTH)
     return fail(err, RT_E_STACK, "BVH depth %d exceeds the traversal stack (%d)", S.max_depth, RT_STACK_DEPTH);
   const int n = (int)order.size();
@@ -693,7 +702,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   std::vector<int> box_face_pos;  // per box: position in `order` of its first face
   {
     bool want = true;
-    if (const char* e = std::getenv("RT_AMD_NO_BOX"))  // experiments: every face its own test
+    if (const char* e = rt_knob("RT_AMD_NO_BOX"))  // experiments: every face its own test
       if (atoi(e)) want = false;
     for (int s = 0; s < n_sets && want; ++s) {
       if (!S.flat && !(s == 0 && !prefix.empty())) break;
@@ -852,12 +861,12 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     // later: pawn+fog 544.8 -> 538.7 ms at 70 % (80: 547, 40: 560); its FP32 kernel keeps 55
     // (70: +3.6 %)
     S.leaf_exit_pct64 = !spheres_only && sc->n_media > 0 ? 70 : S.leaf_exit_pct;
-    if (const char* e = std::getenv("RT_AMD_LEAF_EXIT_PCT"))
+    if (const char* e = rt_knob("RT_AMD_LEAF_EXIT_PCT"))
       S.leaf_exit_pct = S.leaf_exit_pct64 = std::max(1, std::min(100, atoi(e)));
     // and the decoupled lane loop's exit (KernelParams::trav_exit_pct): pawn+fog 386 -> 376 ms at
     // 75 %, demo1 49.2 -> 48.5 at 25 %, the bunny flat between 50 and 75
     S.trav_exit_pct = spheres_only ? 25 : sc->n_media > 0 ? 75 : 50;
-    if (const char* e = std::getenv("RT_AMD_TRAV_PCT")) S.trav_exit_pct = std::max(0, std::min(100, atoi(e)));
+    if (const char* e = rt_knob("RT_AMD_TRAV_PCT")) S.trav_exit_pct = std::max(0, std::min(100, atoi(e)));
   }
   S.n_prims = n;
   return RT_OK;
@@ -867,7 +876,7 @@ int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, boo
   int v = flat ? RT_VAR_FLAT : RT_VAR_BVH;
   if (inst) return RT_VAR_BVH | RT_VAR_INST | (noise ? RT_VAR_NOISE : 0) | (n_media > 0 ? RT_VAR_MEDIA : 0) |
                    (mats ? RT_VAR_MATS : 0) | (tex ? RT_VAR_TEX : 0);  // two-level traversal: the decoupled BVH loop
-  if (const char* e = std::getenv("RT_AMD_VARIANT")) {
+  if (const char* e = rt_knob("RT_AMD_VARIANT")) {
     const int f = atoi(e);
     if (!flat && (f == RT_VAR_BVH_LOCKSTEP || f == RT_VAR_BVH)) v = f;  // flat scenes run on any variant
     if (flat && f >= RT_VAR_FLAT && f <= RT_VAR_BVH) v = f;
@@ -877,7 +886,7 @@ int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, boo
   // instantiation exists; env RT_AMD_LEAF_KIND=0 keeps the generic test)
   int leaf = 0;
   if (v == RT_VAR_BVH) leaf = leaf_kind == 1 ? RT_VAR_LEAF_TRI : leaf_kind == 2 ? RT_VAR_LEAF_SPHERE : 0;
-  if (const char* e = std::getenv("RT_AMD_LEAF_KIND"))
+  if (const char* e = rt_knob("RT_AMD_LEAF_KIND"))
     if (atoi(e) == 0) leaf = 0;
   return v | (noise ? RT_VAR_NOISE : 0) | (n_media > 0 ? RT_VAR_MEDIA : 0) | (mats ? RT_VAR_MATS : 0) |
          (tex ? RT_VAR_TEX : 0) | leaf;
@@ -997,7 +1006,7 @@ void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_s
   // shards: 20.7 -> 22.0 ms), so those keep 4.
   int chunk = spp < 4 ? spp : 4;
   if (resident_lanes > 0 && (long long)P.tile_rows * P.cam.width * spp / 16 >= 64 * resident_lanes) chunk = 16;
-  if (const char* env = std::getenv("RT_AMD_CHUNK")) {  // tuning knob for experiments
+  if (const char* env = rt_knob("RT_AMD_CHUNK")) {  // tuning knob for experiments
     int c = std::atoi(env);
     if (c > 0) chunk = c;
   }
@@ -1008,12 +1017,12 @@ void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_s
   // (at most 48: Cornell binary64 at 1 GPU would take 16 items per pixel instead of 23 and as many
   // fewer commit atomics, but runs 1.5 % slower (6.19 vs 6.10 ms, profiles/r3/iso), so 16).
   int big = RT_BIG_CHUNK_MAX, n_big = 0;
-  if (const char* env = std::getenv("RT_AMD_BIG_CHUNK")) big = std::max(1, std::atoi(env));
+  if (const char* env = rt_knob("RT_AMD_BIG_CHUNK")) big = std::max(1, std::atoi(env));
   int tail_items = sizeof(R) == 8 ? RT_TAIL_ITEMS_F64 : RT_TAIL_ITEMS_F32;
-  if (const char* env = std::getenv("RT_AMD_TAIL_ITEMS")) tail_items = std::atoi(env);
+  if (const char* env = rt_knob("RT_AMD_TAIL_ITEMS")) tail_items = std::atoi(env);
   if (two_sizes && chunk < big && tail_items > 0 && resident_lanes > 0 && tile_pixels > 0) {
     long long t = ((long long)tail_items * chunk * resident_lanes + tile_pixels - 1) / tile_pixels;
-    if (const char* env = std::getenv("RT_AMD_TAIL_SAMPLES")) t = std::max(0, std::atoi(env));  // tests
+    if (const char* env = rt_knob("RT_AMD_TAIL_SAMPLES")) t = std::max(0, std::atoi(env));  // tests
     const long long tail = ((t + chunk - 1) / chunk) * chunk;  // tail samples, a multiple of chunk
     if (tail < spp) {
       const long long bulk = spp - tail;
@@ -1044,7 +1053,7 @@ void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_s
   const int slot_pix = two_sizes ? RT_AGG_PIX_FLAT : RT_AGG_PIX_BVH;
   auto spans = [&](int n) { return n > 0 && (RT_POOL - 1 + n - 1) / n + 1 <= slot_pix; };
   bool agg = tile_pixels < (1ll << 24);  // the item's aggregation code shares its tile-pixel word
-  if (const char* env = std::getenv("RT_AMD_AGG")) agg = agg && std::atoi(env) != 0;
+  if (const char* env = rt_knob("RT_AMD_AGG")) agg = agg && std::atoi(env) != 0;
   P.agg_big = agg && spans(n_big);
   P.agg_small = agg && spans(P.n_chunks);
 }

@@ -28,6 +28,9 @@
 #ifndef RT_BLOCK_BVH
 #define RT_BLOCK_BVH 256      // BVH kernel workgroup at 5 waves/SIMD (others: rt_render_kernel.h RT_BLOCK_OF)
 #endif
+// BVH nodes of a scene at most: the FP32 kernels address a node as a 32-bit byte offset
+// node * 64 from the nodes' base (rt_trace.h RT_NODE_SADDR)
+#define RT_MAX_NODES (1 << 26)
 #define RT_STACK_DEPTH 64     // deepest BVH accepted: the LDS stack is sized by the scene's actual depth (deep
                               // trees lower occupancy instead of failing)
 #define RT_MAX_MEDIA 8
@@ -99,8 +102,13 @@
 #define RT_VAR_INST 64         // flag: the scene has instances (two-level traversal; RT_VAR_BVH only)
 #define RT_VAR_LEAF_TRI 128    // flag: every BVH leaf below a BVH node is a static triangle (RT_VAR_BVH, no instances)
 #define RT_VAR_LEAF_SPHERE 256 // flag: ... a static sphere (idem; kernels without media only)
-// workgroup size of a variant's render kernel
-// host choice of variant (rt_build.cpp); env RT_AMD_VARIANT overrides the base for experiments
+// Experiment knobs (rt_build.cpp): the library reads its RT_AMD_* tuning variables (variant,
+// chunking, aggregation, prefix, box groups, LDS staging, ...) only when RT_AMD_EXPERIMENTS is set
+// to a nonzero value — A/B sessions and the tests that compare code paths set it.  Otherwise
+// rt_knob returns null and every caller (a Haskell program with a stray variable in its
+// environment included) gets the measured defaults.
+const char* rt_knob(const char* name);
+// host choice of variant (rt_build.cpp); knob RT_AMD_VARIANT overrides the base for experiments
 int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, bool inst = false, int leaf_kind = 0);
 
 #define RT_KIND_MASK 3

@@ -52,23 +52,9 @@ static_assert((RT_QUEUES & (RT_QUEUES - 1)) == 0 && RT_QUEUES <= 8, "RT_QUEUES: 
 // wave only.  Pools the host did not qualify (a phase with few chunks per pixel, the pool that
 // straddles the two item sizes) or that find every slot busy commit directly, as before.  Integer
 // sums: the image is bit-identical either way.
-static_assert(RT_POOL >= 64, "a refill must cover every lane of a wave");
-#ifndef RT_AGG_CODE_LOCAL
-#define RT_AGG_CODE_LOCAL 0  // 1: (slot << 5 | pixel) + 1, resolved at the item start: no faster (Cornell f64 5.77 vs 5.74 ms, f32 3.41 vs 3.38; profiles/r3/agg)
-#endif
-static_assert(RT_AGG_PIX_FLAT <= 32 && RT_AGG_PIX_BVH <= 32 && (RT_AGG_SLOTS_FLAT - 1) * 32 + RT_AGG_PIX_FLAT <= 255 &&
-                  (RT_AGG_SLOTS_BVH - 1) * 32 + RT_AGG_PIX_BVH <= 255,
-              "(slot << 5 | pixel) + 1 must fit the 8 bits of rt_trace.h ItemCtx::tp");
-// The dynamic ids [offset, n_items) are split into RT_QUEUES contiguous ranges, each with its own
-// head word (256 B apart): a wave starts on queue (wave % RT_QUEUES) and moves to the next one
-// when its queue is spent, so each word sees 1 / RT_QUEUES of the refills.  Measured (kernel ms,
-// 1 / 2 / 4 / 8 queues): README 0.315 / 0.282 / 0.285 / 0.29 (its cheap samples ran the single
-// word near its returning-atomic rate), README on 2 GPUs 0.191 / 0.189 / 0.177 / 0.180, Cornell
-// 3.455 / 3.42 / 3.42 / 3.43, Cornell's 8-GPU share 0.520 / 0.517 / 0.517 / 0.519.
-#ifndef RT_QUEUES
-#define RT_QUEUES 4
-#endif
-static_assert((RT_QUEUES & (RT_QUEUES - 1)) == 0 && RT_QUEUES <= 8, "RT_QUEUES: a power of two, at most 8 (workspace)");
+// (keeping the item's pixel offset within the slot in its code, resolved at the item's start
+// instead of one LDS read at its commit, measured no faster: Cornell f64 5.77 vs 5.74 ms)
+static_assert(RT_AGG_SLOTS_FLAT < 255 && RT_AGG_SLOTS_BVH < 255, "slot + 1 must fit the 8 bits of rt_trace.h ItemCtx::tp");
 
 // LDS of the aggregation slots per wave: kSlots x kPix x RT_ACC_WORDS words + 2 kSlots header ints
 template <int kSlots, int kPix>
@@ -200,47 +186,35 @@ struct WaveWork {
       if (A.lo[c]) atomicAdd(a + 3 + c, A.lo[c]);
 #endif
   }
-  // an item's tile pixel tagged with its slot code in bits 24-31 (rt_trace.h ItemCtx::tp): 0 for
-  // direct commits, else (slot << 5 | pixel within the slot) + 1 — the slot offset is resolved at
-  // the item's start, so its commit needs no LDS read before the adds
+  // an item's tile pixel tagged with its slot code in bits 24-31 (rt_trace.h ItemCtx::tp): slot +
+  // 1, or 0 for direct commits.  The code exists only in launches that aggregate (P.agg_big |
+  // P.agg_small, set by the host for tiles below 2^24 pixels); elsewhere the word is the plain tile
+  // pixel, whose bits 24-30 may be set (tiles up to 2^31 pixels), and commit must not decode it
+  __device__ __forceinline__ bool aggregating() const { return kSlots > 0 && (P.agg_big | P.agg_small) != 0; }
   __device__ __forceinline__ int tag(int tp, int slot) const {
     if (slot < 0) return tp;
-#if RT_AGG_CODE_LOCAL
-    return tp | ((((slot << 5) | (tp - hdr[kSlots + slot])) + 1) << 24);
-#else
     return tp | ((slot + 1) << 24);
-#endif
   }
   template <class AccT>
   __device__ __forceinline__ void commit(bool c, int tpk, const AccT& acc, bool bad) {
     if (!c) return;
-    const int code = (int)((uint32_t)tpk >> 24);
+    const int code = aggregating() ? (int)((uint32_t)tpk >> 24) : 0;
     const int tp = code ? tpk & 0xffffff : tpk;
     const Acc A = acc_words(acc);
-#ifdef RT_EXP_NO_COMMIT  // ablation: drop the sums (wrong image), measures the cost of the atomics
-    if (A.hi[0] == 12345)
-#endif
-    {
-      if (kSlots == 0 || code == 0) {
-        direct(tp, A);
-      } else {
-#if RT_AGG_CODE_LOCAL
-        const int s = (code - 1) >> 5;
-        unsigned long long* w = slots + s * AggGeom<kSlots, kPix>::kWords + ((code - 1) & 31) * RT_ACC_WORDS(real);
-#else
-        const int s = code - 1;
-        unsigned long long* w = slots + s * AggGeom<kSlots, kPix>::kWords + (tp - hdr[kSlots + s]) * RT_ACC_WORDS(real);
-#endif
+    if (code == 0) {
+      direct(tp, A);
+    } else {
+      const int s = code - 1;
+      unsigned long long* w = slots + s * AggGeom<kSlots, kPix>::kWords + (tp - hdr[kSlots + s]) * RT_ACC_WORDS(real);
 #pragma unroll
-        for (int k = 0; k < 3; ++k)
-          if (A.hi[k]) lds_add(w + k, (unsigned long long)A.hi[k]);
+      for (int k = 0; k < 3; ++k)
+        if (A.hi[k]) lds_add(w + k, (unsigned long long)A.hi[k]);
 #if RT_F64
 #pragma unroll
-        for (int k = 0; k < 3; ++k)
-          if (A.lo[k]) lds_add(w + 3 + k, A.lo[k]);
+      for (int k = 0; k < 3; ++k)
+        if (A.lo[k]) lds_add(w + 3 + k, A.lo[k]);
 #endif
-        __hip_atomic_fetch_add(hdr + s, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // no return
-      }
+      __hip_atomic_fetch_add(hdr + s, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // no return
     }
     if (bad) atomicOr(P.nanflag + tp, 1u);
   }
@@ -274,9 +248,10 @@ struct WaveWork {
 //    [depth][lane] followed by the top P.lds_nodes nodes.  The default decouples traversal
 //    from shading per lane (rt_trace.h lane_loop_bvh); the lockstep loop runs every query of a
 //    segment with the whole wave (kept for experiments; images are bit-identical).
-// Register budget: occupancy floor (waves per SIMD).  Flat: 7 (72 VGPRs, no spills; 2.8%
-// faster on the Cornell box than the 6 it fits unforced, 8 spills and is slower); flat with
-// noise textures: 5.  BVH: 5 (96 VGPRs; faster than 4 on the bunny, pawn and demo1 scenes).
+// Register budget: occupancy floor (waves per SIMD), per kernel class and precision — the table
+// below (RT_WAVES_OF): FP32 flat 7 (5 with noise textures), FP32 BVH 6 without media and constant
+// textures, else 5; binary64 flat 4 / 2, binary64 BVH 4, 3 with media.  Each entry was measured
+// against its neighbours.
 #ifndef RT_WAVES_FLAT
 #define RT_WAVES_FLAT 7
 #endif

@@ -106,6 +106,7 @@ extern thread_local long long counters[4];
 #undef RT_RCP
 #undef RT_RCP_NZ
 #undef RT_SQRT
+#undef RT_NODE_F32
 #if RT_F64
 // binary64: IEEE division and square root, libm / OCML transcendentals (the oracle's libm calls)
 #define RT_NS rtk64
@@ -179,7 +180,6 @@ __device__ __forceinline__ double sqrt_nonneg(double x) {
   s = __builtin_fma(d, h, s);
   return x == 0.0 || x == __builtin_huge_val() ? x : s;
 }
-#ifndef RT_SINCOS_POLY
 // sin / cos of 2 pi u for u in [0, 1) (the samplers' angles; u has 24 random bits): u = k / 128 +
 // b with k = rint(128 u) and |b| <= 1/256 exact, (sin, cos)(2 pi k / 128) from a correctly rounded
 // table (rt_sincos_table.h, 2 KB, L1-resident), sin / cos (2 pi b) by short Taylor polynomials
@@ -200,39 +200,6 @@ __device__ __forceinline__ void sincos_turns(double u, double* sn, double* cs) {
   *sn = __builtin_fma(sa, cb, ca * sb);
   *cs = __builtin_fma(ca, cb, -(sa * sb));
 }
-#else
-// sin / cos of 2 pi u for u in [0, 1) (the samplers' angles; u has 24 random bits): the quadrant
-// q = rint(4 u) and r = u - q / 4 in [-1/8, 1/8] are exact, sin / cos (2 pi r) are Taylor
-// polynomials in r (truncation < 1e-18), and the quadrant swaps / negates them
-__device__ __forceinline__ void sincos_turns(double u, double* sn, double* cs) {
-  const double q = __builtin_rint(4.0 * u);
-  const double r = __builtin_fma(q, -0.25, u);
-  const double r2 = r * r;
-  double ps = 0.10422916220813978;
-  ps = __builtin_fma(ps, r2, -0.7181223017785001);
-  ps = __builtin_fma(ps, r2, 3.8199525848482803);
-  ps = __builtin_fma(ps, r2, -15.094642576822984);
-  ps = __builtin_fma(ps, r2, 42.058693944897634);
-  ps = __builtin_fma(ps, r2, -76.70585975306136);
-  ps = __builtin_fma(ps, r2, 81.60524927607504);
-  ps = __builtin_fma(ps, r2, -41.341702240399755);
-  ps = __builtin_fma(ps, r2, 6.283185307179586);
-  const double sv = r * ps;
-  double pc = 0.282005968455791;
-  pc = __builtin_fma(pc, r2, -1.7143907110886711);
-  pc = __builtin_fma(pc, r2, 7.903536371318465);
-  pc = __builtin_fma(pc, r2, -26.426256783374388);
-  pc = __builtin_fma(pc, r2, 60.24464137187664);
-  pc = __builtin_fma(pc, r2, -85.45681720669371);
-  pc = __builtin_fma(pc, r2, 64.93939402266828);
-  pc = __builtin_fma(pc, r2, -19.739208802178716);
-  pc = __builtin_fma(pc, r2, 1.0);
-  const int k = (int)q & 3;
-  const double ss = (k & 1) ? pc : sv, cc = (k & 1) ? sv : pc;
-  *sn = (k & 2) ? -ss : ss;
-  *cs = ((k + 1) & 2) ? -cc : cc;
-}
-#endif
 }  // namespace rt_math64
 #endif
 #endif
@@ -356,7 +323,7 @@ struct u4 {
   uint32_t x, y, z, w;
 };
 // a ^ b ^ c in one VALU instruction: gfx950's three-input bit operation (truth table 0x96)
-#if defined(RT_HOST_EMU) || defined(RT_EXP_XOR2)
+#ifdef RT_HOST_EMU
 #define RT_XOR3(a, b, c) ((a) ^ (b) ^ (c))
 #else
 #define RT_XOR3(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x96)
@@ -365,7 +332,7 @@ RT_FN u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
 #ifndef RT_PHILOX_ROUNDS
 #define RT_PHILOX_ROUNDS 10
 #endif
-#if !defined(RT_HOST_EMU) && !defined(RT_EXP_HOIST_KEYS)
+#ifndef RT_HOST_EMU
   // the round keys are two scalar adds per round: recompute them at every call instead of
   // letting the compiler keep all twenty live (and spilled) across the lane loop
   asm volatile("" : "+s"(k0), "+s"(k1));
@@ -396,12 +363,7 @@ RT_FN f3 unit_vector(uint32_t a, uint32_t b) {
   real z = RL(1.0) - RL(2.0) * u01(a);
   real r = RT_SQRT(RMAX(RL(0.0), RL(1.0) - z * z));
   real s, c;
-#ifdef RT_EXP_NO_SINCOS  // ablation: wrong directions, measures the cost of sincos
-  c = RL(1.0) - RL(2.0) * u01(b);
-  s = RT_SQRT(RMAX(RL(0.0), RL(1.0) - c * c));
-#else
   RT_SINCOS_TURNS(u01(b), &s, &c);
-#endif
   return mk3(r * c, r * s, z);
 }
 
@@ -735,13 +697,9 @@ RT_FN void test_box(const RT_CAS DevBox* B, const RayCtx& R, real tmin_up, Close
 #endif
     const real s = dot(ax[k], oc);
     const real t0 = -s * inv, t1 = RFMA(-s, inv, inv);  // the s = 0 and s = 1 planes
-#ifndef RT_EXP_FLIP_CMP
     // entering through the s = 1 end: t1 - t0 = inv, so t1 < t0 iff inv < 0 (the sign bit; the
     // two differ only when rounding makes t1 == t0, a slab |s| >= 2^52 box widths away)
     flip[k] = (int)(__builtin_bit_cast(ureal, inv) >> (8 * sizeof(real) - 1));
-#else
-    flip[k] = t1 < t0 ? 1 : 0;
-#endif
     lo[k] = RMIN(t0, t1);
     hi[k] = RMAX(t0, t1);
   }
@@ -1087,9 +1045,6 @@ RT_FN void trav_begin(TravState& S, int root, real tmin) {
 }
 RT_FN bool trav_done(const TravState& S) { return S.node == RT_EMPTY_ROOT && S.leaf == 0; }
 
-#ifndef RT_NODE_FETCH_UNIFORM  // 1: measured slower (pawn+fog +8.5 % FP32, whose BVH is mostly staged)
-#define RT_NODE_FETCH_UNIFORM 0
-#endif
 // FP32 kernels read global nodes at a 32-bit offset from the uniform base (bunny-Cornell -0.3 %,
 // demo1 -1.5 %, pawn+fog -1.0 %); the binary64 kernels keep 64-bit addresses (demo1 +2.4 % with
 // the offsets, bunny and pawn+fog -0.9 %: profiles/r3/fetch)
@@ -1160,14 +1115,9 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
     v4f n0, n1, n2;
     int cl, cr;
     const int node = S.node;
-#if RT_NODE_FETCH_UNIFORM
-    // wave-uniform source: LDS only when every stepping lane's node is staged, else every lane reads
-    // global memory (the staged nodes are there too) — a mixed wave would run both paths, the LDS
-    // reads waiting for the global loads that target the same registers
-    const bool from_lds = !RT_ANY(node >= P.lds_nodes);
-#else
+    // (a wave-uniform source — LDS only when every stepping lane's node is staged — measured
+    // slower: pawn+fog +8.5 % FP32)
     const bool from_lds = node < P.lds_nodes;
-#endif
     if (from_lds) {  // top levels of the surface BVH, staged in LDS per workgroup
       const v4f* nd = W.lds_nodes + 4 * node;
       n0 = nd[0];
@@ -1177,7 +1127,8 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
       cr = RT_F2I(nd[3].y);
     } else {
 #if RT_NODE_SADDR
-      // a 32-bit byte offset from the uniform base (node < 2^25): the loads take the scalar-base +
+      // a 32-bit byte offset from the uniform base (node < 2^26: rt_build.cpp refuses larger BVHs,
+      // RT_MAX_NODES): the loads take the scalar-base +
       // vector-offset form, no 64-bit address arithmetic per lane
       cfpf nd = (cfpf)((const RT_CAS char*)P.nodes + ((uint32_t)node << 6));
 #else
@@ -1204,24 +1155,8 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
     real lfar = RMIN(RMIN(RMAX(lx0, lx1), RMAX(ly0, ly1)), RMIN(RMAX(lz0, lz1), S.C.t));
     real rnear = RMAX(RMAX(RMIN(rx0, rx1), RMIN(ry0, ry1)), RMAX(RMIN(rz0, rz1), S.tmin));
     real rfar = RMIN(RMIN(RMAX(rx0, rx1), RMAX(ry0, ry1)), RMIN(RMAX(rz0, rz1), S.C.t));
-#ifdef RT_EXP_DOUBLE_NODE  // (binary64 node test only)  // ablation: the slab tests computed twice (marginal cost of a node visit)
-    {
-      const real e = (real)P.cam.pad;
-      real ax0 = RFMA(n0.x + e, R.idir.x, -R.oidir.x), ax1 = RFMA(n0.y + e, R.idir.x, -R.oidir.x);
-      real ay0 = RFMA(n0.z + e, R.idir.y, -R.oidir.y), ay1 = RFMA(n0.w + e, R.idir.y, -R.oidir.y);
-      real az0 = RFMA(n2.x + e, R.idir.z, -R.oidir.z), az1 = RFMA(n2.y + e, R.idir.z, -R.oidir.z);
-      real bx0 = RFMA(n1.x + e, R.idir.x, -R.oidir.x), bx1 = RFMA(n1.y + e, R.idir.x, -R.oidir.x);
-      real by0 = RFMA(n1.z + e, R.idir.y, -R.oidir.y), by1 = RFMA(n1.w + e, R.idir.y, -R.oidir.y);
-      real bz0 = RFMA(n2.z + e, R.idir.z, -R.oidir.z), bz1 = RFMA(n2.w + e, R.idir.z, -R.oidir.z);
-      lnear = RMIN(lnear, RMAX(RMAX(RMIN(ax0, ax1), RMIN(ay0, ay1)), RMAX(RMIN(az0, az1), S.tmin)));
-      lfar = RMAX(lfar, RMIN(RMIN(RMAX(ax0, ax1), RMAX(ay0, ay1)), RMIN(RMAX(az0, az1), S.C.t)));
-      rnear = RMIN(rnear, RMAX(RMAX(RMIN(bx0, bx1), RMIN(by0, by1)), RMAX(RMIN(bz0, bz1), S.tmin)));
-      rfar = RMAX(rfar, RMIN(RMIN(RMAX(bx0, bx1), RMAX(by0, by1)), RMIN(RMAX(bz0, bz1), S.C.t)));
-    }
-#endif
 #endif
     const bool hl = lnear <= lfar, hr = rnear <= rfar;
-#ifndef RT_BRANCHY_STACK
     {
       // Branch-free step: the stack slots a pop may need (sp-1, sp-2) are read and the far child
       // is written to slot sp (free; slot stack_depth is a spare row) every step, and the next
@@ -1247,27 +1182,6 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
       S.node = next;
       S.sp = nsp;
     }
-#else
-    if (hl && hr) {
-      const bool rfirst = rnear < lnear;
-      const int nearc = rfirst ? cr : cl, farc = rfirst ? cl : cr;
-      if (S.sp < P.stack_depth) {
-        stack[S.sp * stride] = farc;
-        ++S.sp;
-      } else {
-        overflow = 1;
-      }
-      S.node = nearc;
-    } else if (hl || hr) {
-      S.node = hl ? cl : cr;
-    } else {
-      S.node = pop();
-    }
-    if (S.node < 0 && S.node != kDone && S.leaf == 0) {  // park the first leaf, keep descending
-      S.leaf = S.node;
-      S.node = pop();
-    }
-#endif
     // leave the node loop once P.leaf_exit_pct % of its lanes hold a leaf (100: all of them,
     // Aila & Laine's while-while); the rest keep their state and descend in the next round
     if (RT_BALLOT_COUNT(S.leaf != 0) * 100 >= RT_BALLOT_COUNT(true) * P.leaf_exit_pct) break;
@@ -1289,11 +1203,6 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
       else
         test_rec<false, kInst>(P, r, first + k, R, S.tmin, S.tmin_up, S.C, S.inst, S.ord_base);
     }
-#ifdef RT_EXP_DOUBLE_LEAF  // ablation: every leaf tested twice (marginal cost of the leaf tests)
-    for (int k = 0; k < count; ++k)
-      test_rec(P, ld_rec(cf(P.prims) + 16 * (size_t)(first + k)), first + k, R, S.tmin,
-               S.tmin_up + (real)P.cam.pad, S.C);
-#endif
     S.leaf = 0;
     if (S.node < 0 && S.node != kDone) {  // the node we stopped at is a leaf too: test it next
       S.leaf = S.node;
@@ -1330,12 +1239,7 @@ RT_FN_SPEC void closest<true>(const KernelParams& P, cfp prims, int root, int se
   {
     // set comes from the kernel arguments: the ranges are wave-uniform, every loop is scalar
     const DevFlatSet& S = P.flat_sets[set];
-#ifdef RT_EXP_DOUBLE_TEST  // ablation: every flat set is tested twice (marginal cost of the tests)
-    for (int rep = 0; rep < 2; ++rep) {
-    const real tmin_up = float_up(tmin) + (real)rep * P.cam.pad;
-#else
     const real tmin_up = float_up(tmin);
-#endif
     for (int b = S.box_first; b < S.box_end; ++b) test_box<true>((const RT_CAS DevBox*)P.boxes + b, R, tmin_up, C);
     int k = S.first;
     const RT_CAS PrimRec64* rp = (const RT_CAS PrimRec64*)P.flat_recs + k;  // one 64-B scalar load per record
@@ -1343,9 +1247,6 @@ RT_FN_SPEC void closest<true>(const KernelParams& P, cfp prims, int root, int se
     for (; k < S.end_tri; ++k, ++rp) test_static<RT_PRIM_CLASS_TRI>(ld_rec64(rp), R, tmin, tmin_up, C);
     for (; k < S.end_sphere; ++k, ++rp) test_static<RT_PRIM_CLASS_SPHERE>(ld_rec64(rp), R, tmin, tmin_up, C);
     for (; k < S.end; ++k, ++rp) test_rec<true>(P, ld_rec64(rp), k, R, tmin, tmin_up, C);
-#ifdef RT_EXP_DOUBLE_TEST
-    }
-#endif
 #if RT_F64
     if (C.t < kInf) C.prim = C.ord;  // slot = primitive index (flat scenes store prims in slot order)
 #else
@@ -1387,11 +1288,7 @@ RT_FN void camera_ray(const KernelParams& P, uint32_t pix, int sample, uint32_t 
     gy = (int)(pxgy >> 16);
     px = (int)(pxgy & 0xffffu);
   }
-#ifdef RT_EXP_CHEAP_CAMERA  // ablation (wrong image): measures the camera block's Philox cost
-  u4 w0 = u4{pix * 0x9E3779B9u + (uint32_t)sample, pix ^ ((uint32_t)sample * 0x85EBCA6Bu), 0u, 0u};
-#else
   u4 w0 = philox(pix, (uint32_t)sample, 0u, RT_EV_CAMERA0, P.key0, P.key1);
-#endif
   R.time = u01(w0.z);
   f3 origin = ld3(P.cam.center);
   if (P.cam.disk_u[0] != RL(0.0) || P.cam.disk_u[1] != RL(0.0) || P.cam.disk_u[2] != RL(0.0) || P.cam.disk_v[0] != RL(0.0) ||

@@ -58,7 +58,7 @@ def raytrace(settings: CameraSettings, world, seed, device: int = 0, stats: dict
                            out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st)))
     if stats is not None:
         stats.update(upload_ms=st.upload_ms, kernel_ms=st.kernel_ms, total_ms=st.total_ms, samples=st.samples,
-                     bvh_nodes=st.bvh_nodes, max_stack=st.max_stack)
+                     bvh_nodes=st.bvh_nodes, max_stack=st.max_stack, device_allocs=st.device_allocs)
     return out
 
 
@@ -168,7 +168,8 @@ class MultiDeviceScene:
         _lib.check(self._lib.rt_multi_render(self.handle, ctypes.byref(cs), _seed64(seed), ctypes.byref(ex),
                                              out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st)))
         if stats is not None:
-            stats.update(upload_ms=st.upload_ms, kernel_ms=st.kernel_ms, total_ms=st.total_ms, samples=st.samples)
+            stats.update(upload_ms=st.upload_ms, kernel_ms=st.kernel_ms, total_ms=st.total_ms, samples=st.samples,
+                         device_allocs=st.device_allocs)
         return out
 
     def close(self):

@@ -8,16 +8,20 @@ exactly as the reference writes them.  Each returns (CameraSettings, world, StdG
   bunny_cornell  config 4 (composed: Cornell walls + light + images/bunny.obj)
   pawn_fog       config 5 (composed: pawnTest, test/Main.hs:323-344, plus a fog sphere)
   pawn_test      test/Main.hs:323-344 verbatim (`pawn_demo.png`)
+  demo2          test/Main.hs:259-321 verbatim (`demo2.png`; the reference's test entry point,
+                 demoTest = demo2 "test_image.png" 400 250 4)
 """
 from __future__ import annotations
 
+import math
 import os
 
 from .camera import constBackground, defaultCameraSettings, grayFade, sky
 from .core import V3, degrees, mkStdGen, midpoint, norm, sub
 from .geometry import (boundingBox, bvhTree, cuboid, constantMedium, group, parallelogram, pureGeometry, readObj,
                        rotateX, rotateY, scale, sphere, transform, transformVertices, translate, triangleMesh)
-from .material import (checkerTexture, constantTexture, dielectric, isotropic, lambertian, lightSource,
+from .geometry import moving
+from .material import (checkerTexture, constantTexture, dielectric, imageTexture, isotropic, lambertian, lightSource,
                        marbleTexture, metal, mirror, noiseTexture)
 from .core import fromCorners
 
@@ -268,6 +272,72 @@ def box_gallery(width=200, spp=16, depth=50):
     return cornell_settings(width, spp, depth, redirect=True), world, mkStdGen(77)
 
 
+def earthmap():
+    """images/earthmap.jpg as readImage returns it (Ray.hs:241-245: linear RGB), from the decoded
+    8-bit codes committed losslessly as data/earthmap.png (tests/golden/make_earthmap.py)."""
+    from .ray import readImage
+    return readImage(os.path.join(DATA_DIR, "earthmap.png"))
+
+
+def demo2_world(gen, earth):
+    """generateWorld of test/Main.hs:264-303 evaluated with the splitmix StdGen: 20 x 20 ground
+    cuboids of random height (randomR (1, 101) each, i outer, j inner), then 1000 spheres of radius
+    10 at V3 (randomR (0, 165)) points (linear's V3 instance draws x, y, z in turn) in a bvhTree
+    under translate (V3 (-100) 270 395) . rotateY 15 degrees, the large objects, and two media:
+    the camera-enclosing constantMedium 0.0001 (sphere 0 5000) and the blue fog inside the glass
+    sphere `boundary`.  Returns (world, gen')."""
+    ground = lambertian(constantTexture(V3(0.48, 0.83, 0.53)))
+    white = lambertian(constantTexture(V3(0.73, 0.73, 0.73)))
+    boxes = []
+    for i in range(20):
+        for j in range(20):
+            x0, z0 = -1000.0 + i * 100.0, -1000.0 + j * 100.0
+            y1, gen = gen.randomR(1.0, 101.0)
+            boxes.append(cuboid(fromCorners(V3(x0, 0.0, z0), V3(x0 + 100.0, y1, z0 + 100.0))))
+    balls = []
+    for _ in range(1000):
+        p = []
+        for _ in range(3):
+            x, gen = gen.randomR(0.0, 165.0)
+            p.append(x)
+        balls.append(sphere(V3(*p), 10))
+    boundary = sphere(V3(360, 150, 145), 70)
+    large = [
+        lightSource(constantTexture(V3(7, 7, 7))) << parallelogram(*DEMO2_LIGHT),
+        lambertian(constantTexture(V3(0.7, 0.3, 0.1))) << moving(V3(0, 0, 0), V3(30, 0, 0), sphere(V3(400, 400, 200), 50)),
+        dielectric(1.5) << sphere(V3(260, 150, 45), 50),
+        dielectric(1.5) << boundary,
+        metal(1.0, constantTexture(V3(0.8, 0.8, 0.9))) << sphere(V3(0, 150, 145), 50),
+        lambertian(imageTexture(earth)) << transform(translate(V3(400, 0, 400)) @ rotateY(math.pi / 2),
+                                                     sphere(V3(0, 200, 0), 100)),
+        lambertian(marbleTexture(V3(0, 0, 0.05), 4, 0)) << sphere(V3(220, 280, 300), 80),
+    ]
+    world = group([
+        pureGeometry(group([ground << bvhTree(boxes),
+                            white << transform(translate(V3(-100, 270, 395)) @ rotateY(degrees(15)), bvhTree(balls))]
+                           + large)),
+        isotropic(constantTexture(1)) << constantMedium(0.0001, sphere(V3(0, 0, 0), 5000)),
+        isotropic(constantTexture(V3(0.2, 0.4, 0.9))) << constantMedium(0.2, boundary),
+    ])
+    return world, gen
+
+
+DEMO2_LIGHT = (V3(123, 554, 147), V3(300, 0, 0), V3(0, 0, 265))
+
+
+def demo2(width=800, spp=250, depth=4, seed=1234):
+    """test/Main.hs:259-321: demo2 path imageWidth samplesPerPixel maxRecursionDepth, world from
+    mkStdGen 1234 and the generator after it as raytrace's seed.  Defaults: demo2.png's 800 x 800
+    with the reference's own test entry's spp and depth (demoTest: 250, 4); the published image's
+    spp and depth are not stated (tests/test_gpu.py pins them against it)."""
+    world, gen2 = demo2_world(mkStdGen(seed), earthmap())
+    settings = defaultCameraSettings(
+        cs_center=V3(478, 278, -600), cs_lookAt=V3(278, 278, 0), cs_vfov=degrees(40), cs_aspectRatio=1.0,
+        cs_imageWidth=width, cs_samplesPerPixel=spp, cs_maxRecursionDepth=depth, cs_background=constBackground(0),
+        cs_redirectTargets=[(0.25,) + DEMO2_LIGHT])
+    return settings, world, gen2
+
+
 CONFIGS = {
     "readme": readme_scene,
     "cornell": cornell_box,
@@ -280,4 +350,5 @@ CONFIGS = {
     "box_gallery": box_gallery,
     "bunny_instances": bunny_instances,
     "instance_gallery": instance_gallery,
+    "demo2": demo2,
 }

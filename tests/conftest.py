@@ -5,6 +5,10 @@ import sys
 import numpy as np
 import pytest
 
+# the tests that compare code paths set the library's RT_AMD_* knobs, which it reads only with the
+# experiments switch on (rt_internal.h rt_knob; test_host_mirror checks it is ignored without)
+os.environ.setdefault("RT_AMD_EXPERIMENTS", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests", "kernel_emu")):

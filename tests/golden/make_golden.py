@@ -31,6 +31,8 @@ IMAGES = {
     "cornell_box_noisy": ("cornell_box_noisy.png", "sqrt", "same with cs_redirectTargets = [] (README.md:71)"),
     "demo1": ("demo1.png", "sqrt", "test/Main.hs:136-186 (world from newStdGen: not reproducible)"),
     "pawn_demo": ("pawn_demo.png", "srgb", "test/Main.hs:323-344 (seed 55, 500x500, 400 spp, depth 20)"),
+    "demo2": ("demo2.png", "sqrt", "test/Main.hs:259-321 demo2 (world from mkStdGen 1234; 800x800, spp and depth "
+                                   "not stated)"),
 }
 
 

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
     exported = set(re.findall(r"\bT (rt_\w+)", out.stdout))
     assert set(names) <= exported
-    assert L.rt_abi_version() == _lib.ABI_VERSION == 4
+    assert L.rt_abi_version() == _lib.ABI_VERSION == 5
 
 
 def test_host_only_entry_points_without_gpu():
@@ -64,6 +64,7 @@ int main(void) {
   P(rt_camera_settings); O(rt_camera_settings, image_width); O(rt_camera_settings, background_c0);
   O(rt_camera_settings, defocus_angle); O(rt_camera_settings, redirect_targets);
   P(rt_redirect_target); P(rt_exec); O(rt_exec, flags); O(rt_exec, devices); P(rt_stats); O(rt_stats, samples);
+  O(rt_stats, device_allocs);
   return 0;
 }
 """
@@ -98,6 +99,7 @@ def test_record_layouts_match_header():
     assert c["rt_exec"] == ctypes.sizeof(_lib.RtExec)
     assert c["rt_exec.flags"] == _lib.RtExec.flags.offset and c["rt_exec.devices"] == _lib.RtExec.devices.offset
     assert c["rt_stats"] == ctypes.sizeof(_lib.RtStats) and c["rt_stats.samples"] == _lib.RtStats.samples.offset
+    assert c["rt_stats.device_allocs"] == _lib.RtStats.device_allocs.offset
 
 
 def test_render_fails_loudly_without_a_device():
@@ -158,6 +160,22 @@ def test_device_list_validation_before_device():
     assert L.rt_render(ctypes.byref(c), ctypes.byref(sc), 1, ctypes.byref(ex), out.ctypes.data, None) == _lib.RT_E_INVALID
     with pytest.raises(ValueError):
         _lib.exec_struct(precision="bf16")
+
+
+def test_exec_flags_validated_before_device():
+    """rt_exec.flags: an unknown bit, or both 8-bit encodings, is RT_E_INVALID (not a silent choice),
+    before any device is touched."""
+    from raytrace_amd import scenes
+    from raytrace_amd.scene import flatten
+    L = _lib.load()
+    cs, world, seed = scenes.cornell_box(spp=1, width=4)
+    c, sc = _lib.camera_struct(cs), _lib.scene_struct(flatten(world))
+    out = np.zeros((4, 4, 3))
+    for flags, msg in [(0x100, b"unknown"), (2 | 4, b"exclusive"), (1 | 2 | 4, b"exclusive")]:
+        ex = _lib.exec_struct()
+        ex.flags = flags
+        assert L.rt_render(ctypes.byref(c), ctypes.byref(sc), 1, ctypes.byref(ex), out.ctypes.data, None) == _lib.RT_E_INVALID
+        assert msg in L.rt_last_error(), (flags, L.rt_last_error())
 
 
 def test_haskell_binding_offsets_match_header():

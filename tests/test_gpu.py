@@ -371,6 +371,56 @@ def test_multi_device_scene_and_encoded_output(gpu, precision):
     single.close()
 
 
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_multi_device_scene_allocates_once(gpu, precision):
+    """A resident rt_multi_scene keeps its tiles, workspaces, gather and 8-bit buffers, streams and
+    events across renders: the first render allocates (rt_stats.device_allocs > 0), the next ones
+    of the same or a smaller frame allocate nothing, a larger frame grows the buffers once; images
+    bit-identical to the one-device render throughout."""
+    cs, world, seed = scenes.bunny_cornell(width=48, spp=2)
+    a = R.raytrace(cs, world, seed, precision=precision)
+    m = R.MultiDeviceScene(world, [0, 0, 0])
+    st = [{} for _ in range(4)]
+    np.testing.assert_array_equal(m.render(cs, seed, precision=precision, stats=st[0]), a)
+    np.testing.assert_array_equal(m.render(cs, seed, precision=precision, stats=st[1]), a)
+    np.testing.assert_array_equal(m.render(cs, seed, precision=precision, encode="sqrt", stats=st[2]), R.encode8(a, "sqrt"))
+    np.testing.assert_array_equal(m.render(cs, seed, precision=precision, encode="sqrt"), R.encode8(a, "sqrt"))
+    big = cs.replace(cs_imageWidth=64)
+    b = m.render(big, seed, precision=precision, stats=st[3])
+    np.testing.assert_array_equal(b, R.raytrace(big, world, seed, precision=precision))
+    again = {}
+    m.render(big, seed, precision=precision, stats=again)
+    m.render(cs, seed, precision=precision, stats=again)
+    assert st[0]["device_allocs"] >= 4, st  # three tiles and workspaces, the gather
+    assert st[1]["device_allocs"] == 0, st
+    assert st[2]["device_allocs"] == 1, st  # the 8-bit buffer, once
+    assert st[3]["device_allocs"] > 0 and again["device_allocs"] == 0, (st, again)
+    m.close()
+
+
+@pytest.mark.parametrize("name,precision", [("cornell", "f64"), ("cornell", "f32"), ("bunny_cornell", "f64")])
+def test_tile_beyond_2p24_pixels(gpu, oracle_mod, name, precision):
+    """A one-GPU tile of more than 2^24 pixels (4100 x 4100): the item's tile-pixel word then uses
+    bits 24-30, which the commit must not read as an aggregation slot code (rt_render_kernel.h
+    WaveWork::aggregating).  The whole-frame render equals the same frame rendered as two shards of
+    under 2^24 pixels each, bit for bit, and the oracle on sampled pixels."""
+    from raytrace_amd.ray import assemble_shards, render_shard
+    fn = {"cornell": scenes.cornell_box, "bunny_cornell": scenes.bunny_cornell}[name]
+    cs, world, seed = fn(width=4100, spp=1, depth=3)
+    assert 4100 * 4100 > 1 << 24
+    a = R.raytrace(cs, world, seed, precision=precision)
+    tiles = np.stack([render_shard(cs, world, seed, 2, r, 4, precision=precision) for r in range(2)])
+    assert tiles.shape[1] * 4100 < 1 << 24
+    np.testing.assert_array_equal(assemble_shards(tiles, 4100, 4), a)
+    rows = np.array([0, 1, 2047, 4091, 4099])  # the last rows: tile pixels above 2^24
+    pix = (rows[:, None] * 4100 + np.arange(0, 4100, 7)[None, :]).reshape(-1).astype(np.int32)
+    ref = oracle_mod.render(cs, world, seed, mode=oracle_mod.RNG_PHILOX, pixels=pix)
+    got = a.reshape(-1, 3)[pix].astype(np.float64)
+    tol = 1e-9 if precision == "f64" else 1e-3
+    rel = (np.abs(got - ref) / np.maximum(np.abs(ref), 1e-3 if precision == "f64" else 1.0)).max(-1)
+    assert (rel <= tol).mean() >= 0.99, float((rel <= tol).mean())
+
+
 def test_device_list_bvh_scene(gpu):
     cs, world, seed = scenes.bunny_cornell(width=64, spp=4)
     a = R.raytrace(cs, world, seed)

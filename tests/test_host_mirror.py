@@ -197,3 +197,26 @@ def test_encode8_matches_reference_quantisation():
     x = np.array([[[0.0, 0.8, 1.0], [2.0, -1.0, 0.25]]])
     np.testing.assert_array_equal(R.encode8(x, "sqrt"), [[[0, 228, 255], [255, 0, 128]]])
     np.testing.assert_array_equal(R.encode8(np.array([[[0.8, 1.0, 0.0]]]), "srgb"), [[[232, 255, 0]]])
+
+
+def test_experiment_knobs_ignored_without_the_switch(emu_mod, monkeypatch):
+    """The library reads its RT_AMD_* tuning knobs only with RT_AMD_EXPERIMENTS set (rt_internal.h
+    rt_knob): with the switch unset, a scene renders identically whatever knobs a caller's
+    environment holds (host build + kernel logic through the emulator); with it set they act."""
+    from raytrace_amd import scenes
+    cs, world, seed = scenes.bunny_cornell(width=24, spp=4)
+    monkeypatch.delenv("RT_AMD_EXPERIMENTS", raising=False)
+    base = emu_mod.render(cs, world, seed)
+    info = emu_mod.scene_info(world)
+    knobs = {"RT_AMD_NO_BOX": "1", "RT_AMD_NO_PREFIX": "1", "RT_AMD_VARIANT": "1", "RT_AMD_LEAF_MAX": "7",
+             "RT_AMD_LEAF_KIND": "0", "RT_AMD_CHUNK": "3", "RT_AMD_AGG": "0", "RT_AMD_PREFIX_AREA": "0.9",
+             "RT_AMD_LEAF_EXIT_PCT": "90", "RT_AMD_TRAV_PCT": "10", "RT_AMD_NO_ALIAS": "1", "RT_AMD_LDS_NODES": "0"}
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    assert emu_mod.scene_info(world) == info
+    np.testing.assert_array_equal(emu_mod.render(cs, world, seed), base)
+    monkeypatch.setenv("RT_AMD_EXPERIMENTS", "0")
+    assert emu_mod.scene_info(world) == info
+    monkeypatch.setenv("RT_AMD_EXPERIMENTS", "1")  # switched on, the knobs change the host build
+    on = emu_mod.scene_info(world)
+    assert on["prefix"] == 0 and on["boxes"] == 0 and on != info

@@ -2,6 +2,7 @@
 # A/B of experiment libraries (raytrace_amd/_lib/exp/*.so) against the in-tree build over bench
 # configs: bash tools/ab_libs.sh <tag> "<config>:<sim-shards> ..." [steps]
 # REPS=k repeats the base / experiment pair k times in ABAB order (run-to-run noise is ~1 %)
+export RT_AMD_EXPERIMENTS=1  # the library reads RT_AMD_* knobs / RT_AMD_LIB only with this set
 TAG=$1; CFGS=$2; STEPS=${3:-20}
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 for cfg in $CFGS; do

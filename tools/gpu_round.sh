@@ -18,8 +18,11 @@
 #   phase      phase profile (needs raytrace_amd/_lib/exp/librt_amd_prof.so, -DRT_PHASE_PROF)
 #   microbench VALU rate / binary64 math microbenchmarks, built from source here
 #   rehearse   bench.py --gpus 2 / 3 on one GPU, frames bit-identical to N = 1
+#   demo2fit   tools/demo2_fit.py: demo2 at 800 x 800 against the published demo2.png (depth sweep,
+#              renders for the spp estimate)
 # Env: CONFIGS, PRECS, CPS, AB_CFGS, REPS, PROF_STEPS, PYTEST_K, ROUND.  Each GPU step runs under
 # a timeout of its own and the session stops at the first failing step.
+export RT_AMD_EXPERIMENTS=1  # the library reads RT_AMD_* knobs / RT_AMD_LIB only with this set
 set -o pipefail
 TAG=${1:-r3}
 shift
@@ -100,6 +103,8 @@ PY
       timeout -k 10 120 tools/microbench/f64_math_check > "$OUT/f64_math_check.json" || exit 1 ;;
     rehearse)
       bash tools/rehearse_dist.sh "$TAG/rehearse" || exit 1 ;;
+    demo2fit)
+      timeout -k 10 600 python3 -u tools/demo2_fit.py "$OUT/demo2_fit.jsonl" > "$OUT/demo2_fit.log" 2>&1 || { echo "demo2_fit failed"; tail -20 "$OUT/demo2_fit.log"; exit 1; } ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac

@@ -39,7 +39,7 @@ def main():
     for tag, lib in (("base", None), ("exp", exp_lib)):
         d = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"image_ab_{tag}")  # images stay off gpurun_out/
         os.makedirs(d, exist_ok=True)
-        env = dict(os.environ)
+        env = dict(os.environ, RT_AMD_EXPERIMENTS="1")
         env.pop("RT_AMD_LIB", None)
         if lib:
             env["RT_AMD_LIB"] = os.path.abspath(lib)

@@ -1,7 +1,7 @@
 """Phase profile of the decoupled BVH kernel (diagnostic build: tools/build_variant.sh prof
 -DRT_PHASE_PROF): per-wave shader clocks in the front end (items / camera / segment start), the
 traversal rounds and shading, and the lane occupancy of each, for one config and precision.
-usage: RT_AMD_LIB=raytrace_amd/_lib/exp/librt_amd_prof.so python tools/phase_prof.py CONFIG [f32|f64] [frames]"""
+usage: RT_AMD_EXPERIMENTS=1 RT_AMD_LIB=raytrace_amd/_lib/exp/librt_amd_prof.so python tools/phase_prof.py CONFIG [f32|f64] [frames]"""
 import ctypes
 import json
 import os

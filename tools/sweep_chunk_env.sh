@@ -1,6 +1,7 @@
 #!/bin/bash
 # Item chunk sweep (RT_AMD_CHUNK) over bench configs and --sim-shards values:
 #   bash tools/sweep_chunk_env.sh "<config>:<shards> ..." "<chunk> ..."
+export RT_AMD_EXPERIMENTS=1  # the library reads RT_AMD_* knobs / RT_AMD_LIB only with this set
 OUT=gpurun_out/chunk; mkdir -p $OUT
 for rep in 1 2; do
 for cfg in $1; do

@@ -2,6 +2,7 @@
 # Sweep env tuning knobs (RT_AMD_*) for one config and precision, 2 repetitions each:
 #   bash tools/sweep_env.sh <tag> <config> <f64|f32> "<K=V,K2=V2> <K=V> ..." [steps]
 # ("base" as an entry = no knob).  Prints kernel ms per frame for every setting.
+export RT_AMD_EXPERIMENTS=1  # the library reads RT_AMD_* knobs / RT_AMD_LIB only with this set
 TAG=$1; CFG=$2; PREC=$3; SETS=$4; STEPS=${5:-5}
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 for rep in 1 2; do

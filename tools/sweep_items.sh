@@ -2,6 +2,7 @@
 # Two-size item sweep: big item samples (RT_AMD_BIG_CHUNK) x tail items per resident lane
 # (RT_AMD_TAIL_ITEMS) over bench configs and --sim-shards values, binary64 unless PREC is set:
 #   bash tools/sweep_items.sh <tag> "<config>:<shards> ..." "<big>:<tail> ..."
+export RT_AMD_EXPERIMENTS=1  # the library reads RT_AMD_* knobs / RT_AMD_LIB only with this set
 OUT=gpurun_out/$1; mkdir -p $OUT
 for rep in 1 2; do
 for cfg in $2; do
