@@ -145,6 +145,7 @@ struct rt_multi_scene {
   // kept across renders (grown when a frame needs more): no allocation after the first render
   std::mutex mu;                           // one render at a time: the buffers below are shared
   std::vector<MultiPart> parts;            // per devices[k]
+  std::vector<char> peer_ok;               // per distinct device: may write the first device's memory
   void* d_gather = nullptr;                // first device: the n tiles in global row order
   size_t gather_cap = 0;
   uint8_t* d_codes = nullptr;              // first device: the 8-bit epilogue's output
@@ -210,7 +211,7 @@ size_t workspace_bytes(size_t tile_pixels, int acc_words, size_t* off_flag, size
 // takes one from the stream-ordered pool (hipMallocAsync / hipFreeAsync)
 template <class R>
 int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex, R* d_out,
-                 void* hip_stream, char* ws_given = nullptr, size_t ws_cap = 0) {
+                 void* hip_stream, char* ws_given = nullptr, size_t ws_cap = 0, int frame_rows = 0) {
   if (int rc = ensure_precision<R>(s)) return rc;
   const DevArrays<R>& A = s->arrays<R>();
   KernelParamsT<R> P;
@@ -246,6 +247,7 @@ int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_
   rt_host_plan_work(P, (long long)A.resident_blocks * rt_render_block((const KernelParamsT<R>*)nullptr, s->variant),
                     (s->variant & RT_VAR_BASE) == RT_VAR_FLAT);
   P.trav_exit_pct = s->trav_exit_pct;
+  P.out_frame_rows = frame_rows;
   HIP_TRY(hipSetDevice(s->device));
   // stream-ordered workspace: fixed-point sums, NaN flags, queue counter (graph-capturable)
   const size_t tile_pixels = (size_t)P.tile_rows * P.cam.width;
@@ -412,13 +414,17 @@ int multi_create(const std::shared_ptr<const HostScene>& H, const int32_t* devic
     multi_destroy(M);
     return fail(RT_E_HIP, "stream on device %d", devices[0]);
   }
-  // the first device gathers the shard tiles: let every other device write into its memory
-  // over xGMI (peer access; without it HIP stages the copies itself)
+  // the first device holds the frame: every other device's resolve writes its rows there over
+  // xGMI (peer access); a device without peer access renders into its own tile, which is then
+  // copied over (HIP stages such copies itself)
+  M->peer_ok.assign(distinct.size(), 1);
   for (size_t j = 1; j < distinct.size(); ++j) {
     int can = 0;
+    M->peer_ok[j] = 0;
     if (hipDeviceCanAccessPeer(&can, distinct[j], distinct[0]) == hipSuccess && can) {
       (void)hipSetDevice(distinct[j]);
-      (void)hipDeviceEnablePeerAccess(distinct[0], 0);  // hipErrorPeerAccessAlreadyEnabled is fine
+      const hipError_t e = hipDeviceEnablePeerAccess(distinct[0], 0);
+      M->peer_ok[j] = e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
       (void)hipGetLastError();
     }
   }
@@ -538,15 +544,21 @@ int multi_render(rt_multi_scene* M, const rt_camera_settings* cs, uint64_t seed,
           if (int r = ensure_precisions(s, f32 ? 1 : 2)) return r;
           p.prep_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp).count();
           const size_t tile_pixels = (size_t)p.rows * cs->image_width;
-          if (int r = grow(&q.d_tile, &q.tile_cap, tile_pixels * 3 * esize, &p.allocs)) return r;
+          // n > 1: the resolve writes the shard's rows straight into the frame on the first device
+          // (over xGMI from a peer); without peer access, a tile and a strided copy
+          const bool direct = n > 1 && M->peer_ok[M->scene_of[k]];
+          if (!direct)
+            if (int r = grow(&q.d_tile, &q.tile_cap, tile_pixels * 3 * esize, &p.allocs)) return r;
           const size_t wsb = workspace_bytes(tile_pixels, f32 ? RT_ACC_WORDS(float) : RT_ACC_WORDS(double), nullptr, nullptr);
           if (int r = grow((void**)&q.ws, &q.ws_cap, wsb, &p.allocs)) return r;
+          void* dst = direct ? M->d_gather : q.d_tile;
+          const int frame_rows = direct ? h : 0;
           HIP_TRY(hipEventRecord(q.e0, q.st));
-          const int r = f32 ? render_async<float>(s, cs, seed, &p.ex, (float*)q.d_tile, q.st, q.ws, q.ws_cap)
-                            : render_async<double>(s, cs, seed, &p.ex, (double*)q.d_tile, q.st, q.ws, q.ws_cap);
+          const int r = f32 ? render_async<float>(s, cs, seed, &p.ex, (float*)dst, q.st, q.ws, q.ws_cap, frame_rows)
+                            : render_async<double>(s, cs, seed, &p.ex, (double*)dst, q.st, q.ws, q.ws_cap, frame_rows);
           if (r) return r;
           HIP_TRY(hipEventRecord(q.e1, q.st));
-          if (n > 1) {
+          if (n > 1 && !direct) {
             // shard-local row block b is global block b n + k: one strided copy into the first
             // device's framebuffer (peer-to-peer over xGMI for another device)
             const size_t w = (size_t)rb * row_bytes;

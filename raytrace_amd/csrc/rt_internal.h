@@ -302,6 +302,11 @@ struct KernelParamsT {
   DevCameraT<R> cam;
   uint32_t key0, key1;
   int n_shards, shard, row_block, tile_rows;
+  // resolve target: 0 = `out` holds the shard's tile (tile_rows x width, shard-compact); otherwise
+  // `out` is the WHOLE frame of out_frame_rows rows (a multi-device scene's gather buffer on the
+  // first device, written across xGMI by peer devices) and the resolve puts each tile row at its
+  // global row, so no separate gather copy is needed (rt_api.hip multi_render)
+  int out_frame_rows;
   FastDiv div_width, div_block;  // image width, row block
 };
 using DevMaterial = DevMaterialT<float>;

@@ -367,13 +367,24 @@ void rt_render_kernel(KernelParams P) {
 // mean over spp (Ray.hs:232) from the fixed-point sums; NaN where a sample was non-finite.  One
 // thread per output word (blockIdx.y = the channel) and the FP32 scale from the host: the kernel
 // needs at most 8 VGPRs, so with two streams it fits beside the next frame's 7-wave FP32 render
-// grid (69 VGPRs, 8 left per SIMD lane) instead of waiting for that grid to drain
+// grid (69 VGPRs, 8 left per SIMD lane) instead of waiting for that grid to drain.  frame_rows > 0:
+// `out` is the whole frame and tile row t goes to its global row (the rt_exec row interleave; rows
+// past the image are padding and are skipped) — a multi-device scene's shards resolve straight into
+// the first device's frame over xGMI instead of being gathered by copies afterwards
 __global__ __launch_bounds__(256) void rt_resolve_kernel(const long long* __restrict__ accum,
                                                          const unsigned int* __restrict__ nanflag,
-                                                         real* __restrict__ out, int n_pixels, int spp, double scale) {
+                                                         real* __restrict__ out, int n_pixels, int spp, double scale,
+                                                         int width, int frame_rows, int n_shards, int shard,
+                                                         int row_block) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n_pixels) return;
-  const size_t w = 3 * (size_t)i + blockIdx.y;
+  size_t w = 3 * (size_t)i + blockIdx.y;
+  if (frame_rows > 0) {
+    const int t = i / width, px = i - t * width;
+    const int g = ((t / row_block) * n_shards + shard) * row_block + t % row_block;
+    if (g >= frame_rows) return;
+    w = 3 * ((size_t)g * width + px) + blockIdx.y;
+  }
   const bool bad = nanflag[i] != 0u;
 #if RT_F64
   // (hi + lo 2^-32) 2^-32 / spp: the integer words are exact in binary64 (< 2^53), one rounding
@@ -384,7 +395,7 @@ __global__ __launch_bounds__(256) void rt_resolve_kernel(const long long* __rest
   out[w] = bad ? __builtin_nan("") : sum / (double)spp;
 #else
   (void)spp;
-  out[w] = bad ? __builtin_nanf("") : (float)((double)accum[w] * scale);  // scale = 2^-32 / spp
+  out[w] = bad ? __builtin_nanf("") : (float)((double)accum[3 * (size_t)i + blockIdx.y] * scale);  // scale = 2^-32 / spp
 #endif
 }
 
@@ -520,6 +531,7 @@ int rt_launch_resolve(const KernelParamsT<RT_NS::real>& p, void* stream) {
   int n = p.tile_rows * p.cam.width;
   if (n <= 0) return 0;
   hipLaunchKernelGGL(rt_resolve_kernel, dim3((n + 255) / 256, 3), dim3(256), 0, (hipStream_t)stream,
-                     (const long long*)p.accum, p.nanflag, p.out, n, p.cam.spp, 1.0 / (RT_FIX_SCALE * (double)p.cam.spp));
+                     (const long long*)p.accum, p.nanflag, p.out, n, p.cam.spp, 1.0 / (RT_FIX_SCALE * (double)p.cam.spp),
+                     p.cam.width, p.out_frame_rows, p.n_shards, p.shard, p.row_block);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -650,6 +650,10 @@ RT_FN int box_field(int base, int code, int f, bool& present) {
   present = off != RT_BOX_NO_FACE;
   return base + off;
 }
+// (RT_BOX_EXIT_SKIP=0: the exit face decoded for every lane, as in round 3)
+#ifndef RT_BOX_EXIT_SKIP
+#define RT_BOX_EXIT_SKIP 1
+#endif
 // a face's key order, its primitive and whether the hit on it is valid (margin q >= 0, the face
 // exists, and it is not the face the ray leaves)
 template <bool kInst>
@@ -705,15 +709,25 @@ RT_FN void test_box(const RT_CAS DevBox* B, const RayCtx& R, real tmin_up, Close
   }
   const real tn = RMAX(RMAX(lo[0], lo[1]), lo[2]), tf = RMIN(RMIN(hi[0], hi[1]), hi[2]);
   const int an = lo[0] == tn ? 0 : lo[1] == tn ? 1 : 2;
-  const int af = hi[0] == tf ? 0 : hi[1] == tf ? 1 : 2;
   const int fn = 2 * an + (an == 0 ? flip[0] : an == 1 ? flip[1] : flip[2]);
-  const int ff = 2 * af + 1 - (af == 0 ? flip[0] : af == 1 ? flip[1] : flip[2]);
   const real gap = tf - tn;  // >= 0: the line meets the box
   // the entry point is nearer than the exit point: the exit matters only when the entry is not
   // a valid hit (one key compare per box)
-  int ord_n, ord_f, prim_n = 0, prim_f = 0;
+  int ord_n, ord_f = 0, prim_n = 0, prim_f = 0;
   const bool vn = box_face<kInst>(B, fn, RMIN(gap, tn - tmin_up), R, ord_n, prim_n, !kKeyOnly);
-  const bool vf = box_face<kInst>(B, ff, RMIN(gap, tf - tmin_up), R, ord_f, prim_f, !kKeyOnly);
+  bool vf = false;
+  const real qf = RMIN(gap, tf - tmin_up);
+#if RT_BOX_EXIT_SKIP
+  // ... and then only when the exit itself lies beyond tmin on a met box: rays from inside the box
+  // (the Cornell room) need it, rays outside an object box (hitting its entry face, missing it, or
+  // leaving its surface) do not — a wave-uniform branch skips the exit face's decode for them
+  if (RT_ANY(!vn && qf >= RL(0.0)))
+#endif
+  {
+    const int af = hi[0] == tf ? 0 : hi[1] == tf ? 1 : 2;
+    const int ff = 2 * af + 1 - (af == 0 ? flip[0] : af == 1 ? flip[1] : flip[2]);
+    vf = box_face<kInst>(B, ff, qf, R, ord_f, prim_f, !kKeyOnly);
+  }
   consider<kKeyOnly, kInst>(C, vn ? tn : tf, (vn || vf) ? RL(0.0) : -RL(1.0), vn ? ord_n : ord_f,
                             vn ? prim_n : prim_f, -1);
 }

@@ -67,3 +67,15 @@ def pixel_agreement(img, ref, tol=1e-3):
     """Fraction of pixels whose every channel is within tol (relative above 1) of the oracle."""
     rel = np.abs(img.astype(np.float64) - ref) / np.maximum(1.0, np.abs(ref))
     return float((rel.max(-1) < tol).mean())
+
+
+def record_measure(name, rec):
+    """Append a GPU test's measured figures to gpurun_out/<name>.jsonl (copied to profiles/ by the
+    session): the bars in the tests are derived from these."""
+    d = os.path.join(ROOT, "gpurun_out")
+    try:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, name + ".jsonl"), "a") as f:
+            f.write(json.dumps(rec) + "\n")
+    except OSError:
+        pass

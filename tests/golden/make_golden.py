@@ -6,6 +6,17 @@ Fixtures written (all data, no reference source):
   <name>_block8.npy       8x8-block means of the decoded linear image (float32)
   noise_floor.json        seed-to-seed 8x8-block RMSE of the FP64 oracle at the reference spp
                           (oracle splitmix mode, seeds 234/235 and 100/101)
+  demo1_worlds.json       (--demo1) the spread of demo1's published-image mean over WORLD seeds:
+                          the reference built demo1's world from newStdGen (test/Main.hs:184-185),
+                          so only statistics that do not depend on the world's draw can be pinned;
+                          the FP64 oracle (splitmix) renders worlds 1..8 at 320x180, 64 spp, each
+                          quantised as writeImageSqrt stores it
+  demo2_worlds.json       (--demo2) the same for demo2 (test/Main.hs:259-321): its world IS seeded
+                          (mkStdGen 1234) but the published demo2.png's random ground boxes and
+                          ball cluster are not the ones the restated generator draws (an earlier
+                          revision of the code, like the other PNGs), so its mean is
+                          pinned against the spread over world seeds 1..8 (oracle, splitmix,
+                          160x160, 64 spp, depth 50)
 
 Decoding model (measured on pawn_demo.png's background, whose linear value is analytic):
 the 8-bit code v of a value x in [0,1] is min(255, floor(256 x)) after the transfer
@@ -80,6 +91,44 @@ def main():
                             "oracle_mode": "splitmix"}
         with open(os.path.join(HERE, "noise_floor.json"), "w") as f:
             json.dump(floors, f, indent=1)
+    if "--demo1" in sys.argv:
+        import oracle
+        from raytrace_amd import scenes
+        from raytrace_amd.core import mkStdGen
+        means = []
+        for w in range(1, 9):
+            cs, world, seed = scenes.demo1(width=320, spp=64, seed=w)
+            out = oracle.render(cs, world, seed, mode=oracle.RNG_SPLITMIX, nthreads=os.cpu_count())
+            t = np.sqrt(np.clip(out, 0, 1))
+            lin = decode(np.minimum(np.floor(t * 256), 255), "sqrt")
+            means.append(lin.reshape(-1, 3).mean(0).tolist())
+            print("world", w, means[-1], flush=True)
+        m = np.array(means)
+        with open(os.path.join(HERE, "demo1_worlds.json"), "w") as f:
+            json.dump({"world_seeds": list(range(1, 9)), "width": 320, "height": 180, "spp": 64, "depth": 50,
+                       "oracle_mode": "splitmix", "quantised_linear_mean": means,
+                       "mean_over_worlds": m.mean(0).tolist(), "std_over_worlds": m.std(0, ddof=1).tolist()}, f,
+                      indent=1)
+    if "--demo2" in sys.argv:
+        import oracle
+        from raytrace_amd import scenes
+        from raytrace_amd.core import mkStdGen
+        means = []
+        earth = scenes.earthmap()
+        for w in range(1, 9):
+            world, gen2 = scenes.demo2_world(mkStdGen(w), earth)
+            cs, _, _ = scenes.demo2(width=160, spp=64, depth=50)
+            out = oracle.render(cs, world, gen2, mode=oracle.RNG_SPLITMIX, nthreads=os.cpu_count())
+            t = np.sqrt(np.clip(out, 0, 1))
+            lin = decode(np.minimum(np.floor(t * 256), 255), "sqrt")
+            means.append(lin.reshape(-1, 3).mean(0).tolist())
+            print("world", w, means[-1], flush=True)
+        m = np.array(means)
+        with open(os.path.join(HERE, "demo2_worlds.json"), "w") as f:
+            json.dump({"world_seeds": list(range(1, 9)), "width": 160, "height": 160, "spp": 64, "depth": 50,
+                       "oracle_mode": "splitmix", "quantised_linear_mean": means,
+                       "mean_over_worlds": m.mean(0).tolist(), "std_over_worlds": m.std(0, ddof=1).tolist()}, f,
+                      indent=1)
     print("ok")
 
 

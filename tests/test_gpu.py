@@ -24,7 +24,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, as_published, block8, pixel_agreement
+from conftest import GOLDEN, as_published, block8, pixel_agreement, record_measure
 
 pytestmark = pytest.mark.gpu
 
@@ -40,6 +40,7 @@ CASES = [
     ("bunny_cornell", scenes.bunny_cornell, dict(width=80, spp=8), 0.99, 15.0),
     ("pawn_fog", scenes.pawn_fog, dict(width=80, spp=8), 0.99, 1.0),
     ("pawn_test", scenes.pawn_test, dict(width=80, spp=8), 0.99, 1.0),
+    ("demo2", scenes.demo2, dict(width=96, spp=8), 0.95, 7.0),
 ]
 
 
@@ -100,6 +101,7 @@ FULL = [
     ("bunny_cornell", scenes.bunny_cornell, dict(spp=4), "cornell", 15.0),
     ("pawn_fog", scenes.pawn_fog, dict(spp=4), "cornell", 1.0),
     ("bunny_instances", scenes.bunny_instances, dict(spp=4, n=8), "cornell", 15.0),
+    ("demo2", scenes.demo2, dict(spp=4), "cornell", 7.0),
 ]
 
 
@@ -114,7 +116,7 @@ def test_full_resolution_parity_on_row_subset(gpu, oracle_mod, name, fn, kw, fl,
     rows = np.arange(0, h, 8)
     pix = (rows[:, None] * w + np.arange(w)[None, :]).reshape(-1).astype(np.int32)
     ref = oracle_mod.render(cs, world, seed, mode=oracle_mod.RNG_PHILOX, pixels=pix).reshape(len(rows), w, 3)
-    need = 0.97 if name.startswith("demo1") else 0.99
+    need = 0.97 if name.startswith("demo1") else 0.95 if name == "demo2" else 0.99
     assert_parity(img[rows], ref, precision, need, _floor()[fl], name, kw["spp"], lmax)
 
 
@@ -164,6 +166,76 @@ def test_pawn_demo_matches_published_render(gpu, golden_stats):
     np.testing.assert_allclose(lin.reshape(-1, 3).mean(0), stats["images"]["pawn_demo"]["linear_mean"], rtol=0.01)
     gold = np.load(os.path.join(GOLDEN, "pawn_demo_block8.npy")).astype(np.float64)
     assert np.sqrt(((block8(lin) - gold) ** 2).mean()) < 0.02
+
+
+def test_demo2_matches_published_render(gpu, golden_stats):
+    """demo2 (test/Main.hs:259-321, the reference's test entry point demoTest) against its published
+    demo2.png, 800 x 800.  The render is pinned where the image does not depend on the random world
+    draw: the published ground boxes and ball cluster are not the ones the restated mkStdGen 1234
+    stream draws (an earlier revision of the code, as for the other PNGs), but the light, the back
+    wall seen through the camera-enclosing fog (constantMedium 0.0001 (sphere 0 5000): the
+    ray-starts-inside case of Geometry.hs:313), the moving (motion-blurred) orange sphere and the
+    image-textured earth (imageTexture of images/earthmap.jpg under transform . rotateY) are.
+    Measured against the PNG (tools/demo2_fit.py, profiles/r4/demo2_fit.json): depth 50 and
+    ~10^4 spp (the top band's pixel noise; depth 4, the test entry's, is 0.5-0.8 codes too dark
+    there).  Bars, binary64 at depth 50 and 1000 spp:
+      * linear mean within 3 standard deviations of the spread over world seeds
+        (tests/golden/demo2_worlds.json, FP64 oracle);
+      * 8x8-block RMSE against the PNG in the top band (rows 0-199: light, wall, fog, moving sphere)
+        no larger than between two of our renders with different camera seeds (measured 0.74x), and
+        in the earth's interior within 1.5x of it (measured 1.0-1.1x: the JPEG decoders differ)."""
+    stats, _ = golden_stats
+    with open(os.path.join(GOLDEN, "demo2_worlds.json")) as f:
+        sd = np.array(json.load(f)["std_over_worlds"])
+    pub = np.array(stats["images"]["demo2"]["linear_mean"])
+    gold = np.load(os.path.join(GOLDEN, "demo2_block8.npy")).astype(np.float64)
+    cs, world, seed = scenes.demo2(spp=1000, depth=50)
+    a = as_published(R.raytrace(cs, world, seed), "sqrt")
+    b = as_published(R.raytrace(cs, world, R.mkStdGen(12)), "sqrt")
+    assert a.shape == (800, 800, 3)
+    ba, bb = block8(a), block8(b)
+
+    def rmse(x, y):
+        return np.sqrt(((x - y) ** 2).reshape(-1, 3).mean(0))
+
+    top_pub, top_seed = rmse(ba[:25], gold[:25]), rmse(ba[:25], bb[:25])
+    earth = (slice(52, 64), slice(8, 20))
+    earth_pub, earth_seed = rmse(ba[earth], gold[earth]), rmse(ba[earth], bb[earth])
+    m = a.reshape(-1, 3).mean(0)
+    record_measure("published_renders", dict(test="demo2", mean=m.tolist(), pub=pub.tolist(), world_sd=sd.tolist(),
+                                             top_pub=top_pub.tolist(), top_seed=top_seed.tolist(),
+                                             earth_pub=earth_pub.tolist(), earth_seed=earth_seed.tolist()))
+    assert (np.abs(m - pub) <= 3 * sd).all(), (m, pub, sd)
+    assert (top_pub <= top_seed).all(), (top_pub, top_seed)
+    assert (earth_pub <= 1.5 * earth_seed).all(), (earth_pub, earth_seed)
+
+
+def test_demo1_matches_published_render_statistically(gpu, golden_stats):
+    """demo1 at the reference's 1200 x 675 x 500 against its published demo1.png.  The reference drew
+    the world from newStdGen (test/Main.hs:184-185), so the spheres' placement cannot be reproduced:
+    the quantised image's linear mean must lie within 3 standard deviations of the oracle's spread
+    over world seeds (tests/golden/demo1_worlds.json, make_golden.py --demo1) of the published one,
+    and the 8x8-block RMSE against demo1.png within 1.25x the RMSE between two of our own worlds (the
+    large spheres, ground and sky agree; the small spheres are a different draw either way)."""
+    stats, _ = golden_stats
+    with open(os.path.join(GOLDEN, "demo1_worlds.json")) as f:
+        spread = json.load(f)
+    pub = np.array(stats["images"]["demo1"]["linear_mean"])
+    gold = np.load(os.path.join(GOLDEN, "demo1_block8.npy")).astype(np.float64)
+    lins = []
+    for world_seed in (1, 2):
+        cs, world, seed = scenes.demo1(seed=world_seed)
+        lins.append(as_published(R.raytrace(cs, world, seed), "sqrt"))
+    assert lins[0].shape == (675, 1200, 3)
+    sd = np.array(spread["std_over_worlds"])
+    means = [lin.reshape(-1, 3).mean(0) for lin in lins]
+    rmse_pub = float(np.sqrt(((block8(lins[0]) - gold) ** 2).mean()))
+    rmse_worlds = float(np.sqrt(((block8(lins[0]) - block8(lins[1])) ** 2).mean()))
+    record_measure("published_renders", dict(test="demo1", means=[m.tolist() for m in means], pub=pub.tolist(),
+                                             world_sd=sd.tolist(), rmse_pub=rmse_pub, rmse_worlds=rmse_worlds))
+    for m in means:
+        assert (np.abs(m - pub) <= 3 * sd).all(), (m, pub, sd)
+    assert rmse_pub <= 1.25 * rmse_worlds, (rmse_pub, rmse_worlds)
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])

@@ -34,16 +34,18 @@ import raytrace_amd as R  # noqa: E402
 from raytrace_amd import scenes  # noqa: E402
 from raytrace_amd.camera import image_height  # noqa: E402
 
-# (config, scene fn, row stride, L, per-sample split bound binary64, FP32).  The bounds sit 3-15x
-# above the split rates measured on MI355X (profiles/r3/parity_full_spp.jsonl, implied rate
-# 1 - exact^(1/spp)): binary64 README 0, Cornell 4.4e-7, demo1 1.3e-5 (glass spheres), bunny 3.1e-7,
-# pawn+fog 0; FP32 3.1e-5, 1.7e-5, 8.5e-6, 2.5e-6, 0.
+# (config, scene fn, row stride, L, per-sample split bound binary64, FP32).  Round 4: denser rows
+# (demo1 34, bunny-Cornell 40, pawn+fog 32) and bounds at ~3x the split rates measured on MI355X in
+# round 3 (profiles/r3/parity_full_spp.jsonl, implied rate 1 - exact^(1/spp)): binary64 README 0,
+# Cornell 4.4e-7, demo1 1.34e-5 (glass spheres), bunny 3.1e-7, pawn+fog 0; FP32 3.1e-5, 1.7e-5,
+# 8.5e-6, 2.5e-6, 0.  Where none was measured the bound admits no more than a pixel or a few
+# (README 3e-7 x 50 spp x 50,400 pixels ~ 0.8; pawn+fog 1e-7 x 2000 x 25,600 ~ 5).
 CONFIGS = [
-    ("readme", scenes.readme_scene, 4, 1.0, 1e-6, 1e-4),
-    ("cornell", scenes.cornell_box, 8, 15.0, 5e-6, 1e-4),
-    ("demo1", scenes.demo1, 40, 1.0, 5e-5, 5e-5),
-    ("bunny_cornell", scenes.bunny_cornell, 40, 15.0, 5e-6, 2e-5),
-    ("pawn_fog", scenes.pawn_fog, 100, 1.0, 1e-6, 1e-5),
+    ("readme", scenes.readme_scene, 4, 1.0, 3e-7, 1e-4),
+    ("cornell", scenes.cornell_box, 8, 15.0, 1.3e-6, 5e-5),
+    ("demo1", scenes.demo1, 20, 1.0, 4e-5, 2.5e-5),
+    ("bunny_cornell", scenes.bunny_cornell, 20, 15.0, 1e-6, 7.5e-6),
+    ("pawn_fog", scenes.pawn_fog, 25, 1.0, 1e-7, 1e-6),
 ]
 
 _REF = {}

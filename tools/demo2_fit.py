@@ -76,6 +76,19 @@ def analyse(d):
             b = np.load(os.path.join(d, f"d{depth}_s{s}_k12.npy")).astype(np.float64)
             res[f"pair_{s}"] = float(np.sqrt(((a - b) ** 2).mean()) / np.sqrt(2))
             res[f"a_vs_hi_{s}"] = float(np.sqrt(((a - hi) ** 2).mean()))
+        # the top band (rows 0-199: light, back wall through the fog, the moving sphere) holds no
+        # random geometry: there the PNG differs from the converged render by its own noise only
+        top = slice(0, 200)
+        hi_sig = None
+        a = np.load(os.path.join(d, f"d{depth}_s1000_k11.npy")).astype(np.float64)
+        b = np.load(os.path.join(d, f"d{depth}_s1000_k12.npy")).astype(np.float64)
+        sig1000 = float(np.sqrt(((a[top] - b[top]) ** 2).mean() / 2))
+        hi_sig = sig1000 * np.sqrt(1000 / float(os.environ.get("DEMO2_HI_SPP", "2000")))
+        pub_hi = float(np.sqrt(((pub[top] - hi[top]) ** 2).mean()))
+        sig_pub = float(np.sqrt(max(pub_hi ** 2 - hi_sig ** 2, 1e-9)))
+        res.update(top_rmse_pub_vs_hi=pub_hi, top_sigma_1000=sig1000, top_sigma_pub=sig_pub,
+                   spp_estimate=round(1000 * (sig1000 / sig_pub) ** 2),
+                   top_mean_codes_pub=pub[top].mean((0, 1)).tolist(), top_mean_codes_hi=hi[top].mean((0, 1)).tolist())
         print(json.dumps(res))
 
 if __name__ == "__main__":

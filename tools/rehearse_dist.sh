@@ -19,7 +19,11 @@ a = json.loads(open(f"{out}/n1.json").read().strip().splitlines()[-1])
 print("n1", a["value"], a["check"])
 for n in ns:
     b = json.loads(open(f"{out}/n{n}.json").read().strip().splitlines()[-1])
+    ab = b.get("abi_device_list") or {}
     print(f"n{n}", b["value"], b["n_gpus"], b["check"], b["config"]["parallelism"])
+    print(f"  abi_device_list {ab.get('devices')} {ab.get('ms_per_frame')} ms/frame, sha16 {ab.get('sha16')}, "
+          f"allocs {ab.get('device_allocs_timed')}")
     assert b["n_gpus"] == int(n) and b["check"]["finite"] and b["check"]["sha16"] == a["check"]["sha16"], "mismatch"
+    assert ab.get("sha16") == a["check"]["sha16"] and ab.get("device_allocs_timed") == 0, "abi device list"
 print("rehearsal ok: frames bit-identical to N=1")
 PY
