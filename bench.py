@@ -190,7 +190,7 @@ def roofline_of(config, precision, kernel_ms, launch_ms, share, samples_per_laun
     return r
 
 
-def abi_device_list(world, cs, seed, devices, precision, frames, warmup=2):
+def abi_device_list(world, cs, seed, devices, precision, frames, warmup=2, warmup_s=0.5):
     """The drop-in's own multi-GPU path: ONE process rendering the whole frame through the C ABI's
     device list (rt_multi_scene_create / rt_multi_render: shard k on devices[k], peer-copy gather
     into devices[0], one device-to-host copy), as the Haskell binding calls it (Device.hs passes
@@ -201,8 +201,12 @@ def abi_device_list(world, cs, seed, devices, precision, frames, warmup=2):
     from raytrace_amd.ray import MultiDeviceScene
     m = MultiDeviceScene(world, devices)
     try:
-        for _ in range(warmup):  # uploads, occupancy queries, the resident buffers
+        tw, k = time.perf_counter(), 0
+        # uploads, occupancy queries, the resident buffers; then at least warmup_s of frames (the
+        # ranks that just left the process group may still be tearing down on these devices)
+        while k < warmup or time.perf_counter() - tw < warmup_s:
             m.render(cs, seed, precision=precision, row_block=1)
+            k += 1
         kms, allocs = [], 0
         t0 = time.perf_counter()
         for _ in range(frames):
