@@ -880,14 +880,12 @@ int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, boo
     const int f = atoi(e);
     if (!flat && (f == RT_VAR_BVH_LOCKSTEP || f == RT_VAR_BVH)) v = f;  // flat scenes run on any variant
     if (flat && f >= RT_VAR_FLAT && f <= RT_VAR_BVH) v = f;
-    // the workgroup ray-queue experiment: BVH scenes with constant textures
-    if (!flat && f == RT_VAR_BVH_WG && !tex && !noise) v = f;
   }
-  // one-class BVH leaves: the decoupled kernels (leaf_kind covers the leaves below BVH nodes of the
+  // one-class BVH leaves: the decoupled kernel (leaf_kind covers the leaves below BVH nodes of the
   // surface and media sets; the kernel dispatch keeps the generic test where no one-class
   // instantiation exists; env RT_AMD_LEAF_KIND=0 keeps the generic test)
   int leaf = 0;
-  if (v == RT_VAR_BVH || v == RT_VAR_BVH_WG) leaf = leaf_kind == 1 ? RT_VAR_LEAF_TRI : leaf_kind == 2 ? RT_VAR_LEAF_SPHERE : 0;
+  if (v == RT_VAR_BVH) leaf = leaf_kind == 1 ? RT_VAR_LEAF_TRI : leaf_kind == 2 ? RT_VAR_LEAF_SPHERE : 0;
   if (const char* e = rt_knob("RT_AMD_LEAF_KIND"))
     if (atoi(e) == 0) leaf = 0;
   return v | (noise ? RT_VAR_NOISE : 0) | (n_media > 0 ? RT_VAR_MEDIA : 0) | (mats ? RT_VAR_MATS : 0) |

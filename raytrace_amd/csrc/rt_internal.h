@@ -94,7 +94,6 @@
 #define RT_VAR_FLAT 0          // every set one flat leaf, lockstep lane loop
 #define RT_VAR_BVH_LOCKSTEP 1  // BVH, lockstep lane loop (reference schedule; experiments and tests)
 #define RT_VAR_BVH 2           // BVH, traversal decoupled from shading (default for BVH scenes)
-#define RT_VAR_BVH_WG 3        // BVH, the workgroup's lanes trace each other's rays (experiment; rt_trace.h lane_loop_wg)
 #define RT_VAR_BASE 3
 #define RT_VAR_NOISE 4         // flag: the scene has noise / marble textures (their code compiled in)
 #define RT_VAR_MEDIA 8         // flag: the scene has constantMedium volumes (their code compiled in)

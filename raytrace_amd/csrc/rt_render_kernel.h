@@ -287,25 +287,14 @@ struct WaveWork {
 #ifndef RT_WAVES64_BVH_MEDIA
 #define RT_WAVES64_BVH_MEDIA 3  // the media kernels spill more: pawn+fog 641 ms at 3, 883 at 4
 #endif
-// the workgroup ray-queue experiment (RT_VAR_BVH_WG): a lane holds a parked tracer ray beside its
-// own path's ray while it shades, and the LDS holds every lane's ray slot beside the stacks — one
-// occupancy level below the decoupled kernels (DESIGN §4 "Round 4")
-#ifndef RT_WAVES64_WG
-#define RT_WAVES64_WG 3
-#endif
-#ifndef RT_WAVES_WG
-#define RT_WAVES_WG 4
-#endif
 #if RT_F64
 #define RT_WAVES_OF(kVar, kTex, kMedia, kMats)                                                     \
   ((kVar) == RT_VAR_FLAT ? ((kTex) == 0 && !(kMedia) && !(kMats) ? RT_WAVES64_FLAT_LITE : RT_WAVES64_FLAT) \
-                         : (kVar) == RT_VAR_BVH_WG ? RT_WAVES64_WG                                   \
                          : (kMedia) ? RT_WAVES64_BVH_MEDIA                                          \
                          : ((kTex) == 0 && !(kMats) ? RT_WAVES64_BVH_LITE : RT_WAVES64_BVH))
 #else
 #define RT_WAVES_OF(kVar, kTex, kMedia, kMats)                                                           \
   ((kVar) == RT_VAR_FLAT ? ((kTex) == 2 ? RT_WAVES_FLAT_NOISE : (kTex) == 0 ? RT_WAVES_FLAT_TEX0 : RT_WAVES_FLAT) \
-                         : (kVar) == RT_VAR_BVH_WG ? RT_WAVES_WG                                         \
                          : ((kTex) == 0 && !(kMedia) ? RT_WAVES_BVH_LITE : RT_WAVES_BVH))
 #endif
 // BVH workgroup size of a kernel class: each workgroup stages its own LDS copy of the top BVH
@@ -358,19 +347,6 @@ void rt_render_kernel(KernelParams P) {
     work.finish();
   } else {
     v4f* lds_nodes = reinterpret_cast<v4f*>(smem_rest + (P.stack_depth + 1) * kBlock);
-    // RT_VAR_BVH_WG: the workgroup's ray queue after the stacks, the staged nodes after it
-    constexpr bool kWg = kVar == RT_VAR_BVH_WG;
-    WgQueue Q{};
-    v4f* wg_nodes = lds_nodes;
-    if constexpr (kWg) {
-      char* qb = reinterpret_cast<char*>(lds_nodes);
-      Q = wg_queue_at(qb, kBlock, kMedia, kLeaf == 0);
-      wg_nodes = reinterpret_cast<v4f*>(qb + wg_queue_bytes(kBlock, kMedia, kLeaf == 0));
-      for (int i = threadIdx.x; i < kWgRing; i += kBlock) Q.ring[i] = 0xffffffffu;
-      if (threadIdx.x < 4) Q.ctl[threadIdx.x] = 0u;
-      if (threadIdx.x < (kBlock + 63) / 64) Q.ready[threadIdx.x] = 0ull;
-      lds_nodes = wg_nodes;
-    }
     const float4* src = reinterpret_cast<const float4*>(P.nodes);
     for (int i = threadIdx.x; i < 4 * P.lds_nodes; i += kBlock) {
       const float4 q = src[i];
@@ -379,16 +355,10 @@ void rt_render_kernel(KernelParams P) {
     __syncthreads();
     WaveWork<kSlots, kPix> work(P, wave, waves, agg);
     const Trav W{smem_rest + threadIdx.x, kBlock, lds_nodes};
-    if constexpr (kVar == RT_VAR_BVH_LOCKSTEP) {
+    if constexpr (kVar == RT_VAR_BVH_LOCKSTEP)
       overflow = lane_loop_lockstep<false, kTex, kMedia, kMats>(P, work, W, P.prims, acc);
-    } else if constexpr (kVar == RT_VAR_BVH_WG) {
-      // the queue sits between the stacks and the staged nodes (render_lds_bytes), the nodes after it
-      (void)lds_nodes;
-      overflow = lane_loop_wg<kTex, kMedia, kMats, kLeaf>(P, work, Trav{W.stack, W.stride, wg_nodes}, P.prims, acc, Q,
-                                                          (int)threadIdx.x, wave_in_block);
-    } else {
+    else
       overflow = lane_loop_bvh<kTex, kMedia, kMats, kInst, kLeaf>(P, work, W, P.prims, acc);
-    }
     work.finish();
   }
   if (overflow) atomicOr(P.status, 1);
@@ -430,15 +400,12 @@ __global__ __launch_bounds__(256) void rt_resolve_kernel(const long long* __rest
 }
 
 // the workgroup size of a variant's kernel (RT_BLOCK_OF of its class)
-static int variant_class(int variant) {
-  const int base = variant & RT_VAR_BASE;
-  return base == RT_VAR_FLAT ? RT_VAR_FLAT : base == RT_VAR_BVH_WG ? RT_VAR_BVH_WG : RT_VAR_BVH;
-}
 static int render_block(int variant) {
+  const bool flat = (variant & RT_VAR_BASE) == RT_VAR_FLAT;
   const int tex = (variant & RT_VAR_NOISE) ? 2 : (variant & RT_VAR_TEX) ? 1 : 0;
   const bool media = (variant & RT_VAR_MEDIA) != 0, mats = (variant & RT_VAR_MATS) != 0;
   (void)mats;
-  return RT_BLOCK_OF(variant_class(variant), tex, media, mats);
+  return RT_BLOCK_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats);
 }
 static bool acc_in_lds(int variant) {
   return RT_ACC_LDS_OF((variant & RT_VAR_BASE) == RT_VAR_FLAT ? RT_VAR_FLAT : RT_VAR_BVH, (variant & RT_VAR_MEDIA) != 0);
@@ -450,11 +417,7 @@ static size_t render_fixed_lds(int variant) {
   const size_t agg = (size_t)(flat ? AggGeom<RT_AGG_SLOTS_FLAT, RT_AGG_PIX_FLAT>::kWaveBytes
                                    : AggGeom<RT_AGG_SLOTS_BVH, RT_AGG_PIX_BVH>::kWaveBytes) *
                      (render_block(variant) / 64);
-  const bool generic_leaves = !(variant & (RT_VAR_LEAF_TRI | RT_VAR_LEAF_SPHERE));
-  const size_t queue = (variant & RT_VAR_BASE) == RT_VAR_BVH_WG
-                           ? wg_queue_bytes(render_block(variant), (variant & RT_VAR_MEDIA) != 0, generic_leaves)
-                           : 0;
-  return acc + agg + queue;
+  return acc + agg;
 }
 static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
   return render_fixed_lds(variant) + ((variant & RT_VAR_BASE) == RT_VAR_FLAT
@@ -482,11 +445,11 @@ static render_fn render_kernel_media(int variant) {
   // one-class BVH leaves (RT_VAR_LEAF_*): the decoupled kernel without instances; with media,
   // triangle leaves and constant textures only (pawn+fog)
   if (variant & RT_VAR_MEDIA) {
-    if constexpr ((kVar == RT_VAR_BVH || kVar == RT_VAR_BVH_WG) && !kInst && kTex == 0 && RT_LEAF_MEDIA)
+    if constexpr (kVar == RT_VAR_BVH && !kInst && kTex == 0 && RT_LEAF_MEDIA)
       if (variant & RT_VAR_LEAF_TRI) return render_kernel_mats<kVar, kTex, true, kInst, 1>(variant);
     return render_kernel_mats<kVar, kTex, true, kInst, 0>(variant);
   }
-  if constexpr ((kVar == RT_VAR_BVH || kVar == RT_VAR_BVH_WG) && !kInst) {
+  if constexpr (kVar == RT_VAR_BVH && !kInst) {
     if (variant & RT_VAR_LEAF_TRI) return render_kernel_mats<kVar, kTex, false, kInst, 1>(variant);
     if (variant & RT_VAR_LEAF_SPHERE) return render_kernel_mats<kVar, kTex, false, kInst, 2>(variant);
   }
@@ -504,8 +467,6 @@ static render_fn render_kernel_of(int variant) {
   switch (variant & RT_VAR_BASE) {
     case RT_VAR_FLAT: return render_kernel_flags<RT_VAR_FLAT, false>(variant);
     case RT_VAR_BVH_LOCKSTEP: return render_kernel_flags<RT_VAR_BVH_LOCKSTEP, false>(variant);
-    case RT_VAR_BVH_WG:  // constant textures only (rt_host_variant); no instances
-      return render_kernel_media<RT_VAR_BVH_WG, 0, false>(variant);
     default: return render_kernel_flags<RT_VAR_BVH, false>(variant);
   }
 }
@@ -531,10 +492,11 @@ int rt_render_resident_blocks(const KernelParamsT<RT_NS::real>*, int device, int
 // item sums take per workgroup: the host sizes the LDS node staging to what is left of the
 // workgroup's share of a CU's LDS at that occupancy (rt_api.hip ensure_precision)
 int rt_render_waves(const KernelParamsT<RT_NS::real>*, int variant) {
+  const bool flat = (variant & RT_VAR_BASE) == RT_VAR_FLAT;
   const int tex = (variant & RT_VAR_NOISE) ? 2 : (variant & RT_VAR_TEX) ? 1 : 0;
   const bool media = (variant & RT_VAR_MEDIA) != 0, mats = (variant & RT_VAR_MATS) != 0;
   (void)mats;  // the FP32 occupancy table does not depend on the material set
-  return RT_WAVES_OF(RT_NS::variant_class(variant), tex, media, mats);
+  return RT_WAVES_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats);
 }
 int rt_render_block(const KernelParamsT<RT_NS::real>*, int variant) { return RT_NS::render_block(variant); }
 int rt_render_acc_lds(const KernelParamsT<RT_NS::real>*, int variant) {

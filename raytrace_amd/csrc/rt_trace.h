@@ -45,7 +45,6 @@
 #include <cmath>
 #include <cstring>
 #define RT_FN static inline
-#define RT_HD static inline
 #define RT_FN_SPEC inline  // explicit specialisations take no storage class
 namespace rt_emu {
 inline int f2i(float f) {
@@ -63,7 +62,6 @@ extern thread_local long long counters[4];
 #define RT_CAS
 #else
 #define RT_FN __device__ __forceinline__
-#define RT_HD __host__ __device__ inline
 #define RT_FN_SPEC __device__ __forceinline__
 #define RT_F2I(f) __float_as_int(f)
 #define RT_COUNT(i) ((void)0)
@@ -1802,369 +1800,6 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Work& work, const Trav& TW, const
     RT_PROF_MARK(PF_SHADE);
   }
   RT_PROF_FLUSH
-  return overflow;
-}
-
-// ---------------------------------------------------------------- workgroup ray queue
-// RT_VAR_BVH_WG (round-4 experiment): the lanes of a workgroup trace each other's rays.
-// A lane OWNS one path (item, sample, throughput: as in lane_loop_bvh) and, as a TRACER, holds at
-// most one ray of any of the workgroup's paths.  An owner step shades the owner's paths whose
-// segment results are back, takes items, starts samples and segments, tests a new segment's
-// large-primitive prefix (wave-uniform records) and publishes the ray into its LDS slot and the
-// workgroup's ring of slot ids.  A tracer step pops rays into the lanes that hold none — a lane
-// that finishes a ray takes the next one at once, so the traversal rounds run on full waves while
-// the ring holds rays — and returns each finished segment's result to its owner's slot and ready
-// mask.  A wave leaves its tracer step when enough of its own waiting paths are back
-// (trav_exit_pct %) or nothing is left to trace; rays it still holds stay parked in its registers
-// (their stacks in LDS) until its next tracer step.  Same per-path arithmetic and counters as the
-// other loops: bit-identical images.
-constexpr int kWgRing = 1024;  // ring entries (>= the workgroup's slots): (position & 0x3fffff) << 10 | slot
-struct WgQueue {
-  real* o;          // [3][B]: component k of slot s at o[k * B + s]
-  real* d;          // [3][B]
-  real* t;          // [B] the prefix's closest t (published), then the segment's tbest (result)
-  real* time;       // [B] (generic leaves only: moving primitives)
-  int* self;        // [B] the leaf the ray leaves
-  int* ord;         // [B] the prefix's closest key order
-  int* prim;        // [B] the prefix's closest primitive, then the segment's best (result)
-  int* hitm;        // [B] (media) the segment's hit medium (result)
-  uint32_t* psx;    // [3][B] (media) pix, sample, seg: the medium draws' Philox counter
-  uint32_t* ring;   // [kWgRing]
-  uint32_t* ctl;    // [0] head (next position to pop), [1] tail (next position to push)
-  unsigned long long* ready;  // [B / 64]: bit l of word w = slot 64 w + l has its result back
-  int B;
-};
-// LDS bytes of a workgroup's queue (B slots), and its layout from `base` (16-B aligned)
-RT_HD size_t wg_queue_bytes(int B, bool media, bool time) {
-  size_t n = (size_t)B * (7 + (time ? 1 : 0)) * sizeof(real) + (size_t)B * 4 * (3 + (media ? 4 : 0));
-  n += (size_t)kWgRing * 4 + 16 + (size_t)((B + 63) / 64) * 8;
-  return (n + 15) & ~(size_t)15;
-}
-RT_FN WgQueue wg_queue_at(char* base, int B, bool media, bool time) {
-  WgQueue Q;
-  real* r = reinterpret_cast<real*>(base);
-  Q.o = r;
-  Q.d = r + 3 * B;
-  Q.t = r + 6 * B;
-  Q.time = time ? r + 7 * B : nullptr;
-  int* i = reinterpret_cast<int*>(r + (7 + (time ? 1 : 0)) * B);
-  Q.self = i;
-  Q.ord = i + B;
-  Q.prim = i + 2 * B;
-  Q.hitm = media ? i + 3 * B : nullptr;
-  Q.psx = media ? reinterpret_cast<uint32_t*>(i + 4 * B) : nullptr;
-  uint32_t* u = reinterpret_cast<uint32_t*>(i + (3 + (media ? 4 : 0)) * B);
-  Q.ring = u;
-  Q.ctl = u + kWgRing;
-  Q.ready = reinterpret_cast<unsigned long long*>(u + kWgRing + 4);
-  Q.B = B;
-  return Q;
-}
-RT_FN uint32_t wg_tag(uint32_t pos) { return (pos & 0x3fffffu) << 10; }
-
-#ifdef RT_HOST_EMU
-// the emulator: one lane per wave and per workgroup, so the queue is the lane's own
-RT_FN unsigned long long wg_take_ready(const WgQueue& Q, int w) {
-  const unsigned long long m = Q.ready[w];
-  Q.ready[w] = 0ull;
-  return m;
-}
-RT_FN unsigned long long wg_peek_ready(const WgQueue& Q, int w) { return Q.ready[w]; }
-RT_FN void wg_push(const WgQueue& Q, bool pub, int slot) {
-  if (!pub) return;
-  const uint32_t pos = Q.ctl[1]++;
-  Q.ring[pos & (kWgRing - 1)] = wg_tag(pos) | (uint32_t)slot;
-}
-RT_FN int wg_pop(const WgQueue& Q, bool want) {
-  if (!want || Q.ctl[0] == Q.ctl[1]) return -1;
-  const uint32_t pos = Q.ctl[0]++;
-  return (int)(Q.ring[pos & (kWgRing - 1)] & 1023u);
-}
-RT_FN void wg_set_ready(const WgQueue& Q, int s) { Q.ready[s >> 6] |= 1ull << (s & 63); }
-RT_FN int wg_lane() { return 0; }
-#else
-RT_FN unsigned long long wg_bcast64(unsigned long long v, int leader) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane(__shfl((uint32_t)v, leader));
-  const uint32_t hi = __builtin_amdgcn_readfirstlane(__shfl((uint32_t)(v >> 32), leader));
-  return (unsigned long long)hi << 32 | lo;
-}
-RT_FN unsigned long long wg_take_ready(const WgQueue& Q, int w) {
-  const int leader = __ffsll((unsigned long long)__ballot(true)) - 1;
-  unsigned long long m = 0ull;
-  if ((int)__lane_id() == leader)
-    m = __hip_atomic_exchange(Q.ready + w, 0ull, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  return wg_bcast64(m, leader);
-}
-RT_FN unsigned long long wg_peek_ready(const WgQueue& Q, int w) {
-  const int leader = __ffsll((unsigned long long)__ballot(true)) - 1;
-  unsigned long long m = 0ull;
-  if ((int)__lane_id() == leader) m = __hip_atomic_load(Q.ready + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  return wg_bcast64(m, leader);
-}
-// wave-collective: the lanes with pub append their slot (one returning LDS atomic for the wave)
-RT_FN void wg_push(const WgQueue& Q, bool pub, int slot) {
-  const unsigned long long m = __ballot(pub);
-  if (m == 0ull) return;
-  const int lane = (int)__lane_id();
-  const int leader = __ffsll(m) - 1;
-  uint32_t base = 0;
-  if (lane == leader) base = __hip_atomic_fetch_add(Q.ctl + 1, (uint32_t)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
-  if (pub) {
-    const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    // release: the slot's ray (written before) is visible to whoever pops this entry
-    __hip_atomic_store(Q.ring + (pos & (kWgRing - 1)), wg_tag(pos) | (uint32_t)slot, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-}
-// wave-collective: lanes with want take a slot id each while the ring holds any (-1: none)
-RT_FN int wg_pop(const WgQueue& Q, bool want) {
-  const unsigned long long m = __ballot(want);
-  if (m == 0ull) return -1;
-  const int lane = (int)__lane_id();
-  const int leader = __ffsll(m) - 1;
-  const uint32_t cnt = (uint32_t)__popcll(m);
-  uint32_t h = 0, take = 0;
-  if (lane == leader) {
-    for (;;) {
-      h = __hip_atomic_load(Q.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const uint32_t t = __hip_atomic_load(Q.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const uint32_t avail = t - h;  // < 2^31: at most one pending ray per slot
-      take = avail < cnt ? avail : cnt;
-      if (take == 0u) break;
-      uint32_t expect = h;
-      if (__hip_atomic_compare_exchange_strong(Q.ctl, &expect, h + take, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP))
-        break;
-    }
-  }
-  h = __builtin_amdgcn_readfirstlane(__shfl(h, leader));
-  take = __builtin_amdgcn_readfirstlane(__shfl(take, leader));
-  const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-  if (!want || rank >= take) return -1;
-  const uint32_t pos = h + rank;
-  // the producer reserved this position before writing it: wait for its tag (at most one pending
-  // entry per slot, so the ring never wraps onto an entry not yet read)
-  uint32_t e;
-  do {
-    e = __hip_atomic_load(Q.ring + (pos & (kWgRing - 1)), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  } while ((e & ~1023u) != wg_tag(pos));
-  return (int)(e & 1023u);
-}
-RT_FN void wg_set_ready(const WgQueue& Q, int s) {
-  __hip_atomic_fetch_or(Q.ready + (s >> 6), 1ull << (s & 63), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-RT_FN int wg_lane() { return (int)__lane_id(); }
-#endif
-
-template <int kTex, bool kMedia, bool kMats, int kLeaf, class Work, class AccT>
-RT_FN int lane_loop_wg(const KernelParams& P, Work& work, const Trav& TW, const real* prims_, AccT& acc,
-                       const WgQueue& Q, int slot, int wave_in_block) {
-  constexpr bool kTime = kLeaf == 0;
-  constexpr int ST_WAIT = 5, ST_DONE = 6;
-  const cfp prims = cf(prims_);
-  const int n_media = kMedia ? P.n_media : 0;
-  const int B = Q.B;
-  int overflow = 0;
-  // ---- owner: its path
-  ItemCtx I{-1, 0, 0, 0u, 0u};
-  int seg = 0;
-  bool bad = false;
-  int ost = ST_NEED_ITEM;
-  f3 T = mk3(RL(1.), RL(1.), RL(1.));
-  acc_clear(acc);
-  // ---- tracer: the ray it holds (of any path of the workgroup)
-  bool tr = false;
-  int tslot = 0;
-  RayCtx R;
-  R.o = R.d = mk3(RL(0.), RL(0.), RL(0.));
-#if RT_NODE_F32
-  R.idir = R.off0 = R.off1 = f3n{0.f, 0.f, 0.f};
-#else
-  R.idir = R.oidir = R.o;
-#endif
-  R.time = RL(0.0);
-  R.self_gid = -1;
-  R.self_inst = -1;
-  TravState S;
-  trav_begin(S, RT_EMPTY_ROOT, kTmin);
-  int q = 0, best = -1, hit_medium = -1;
-  real tbest = kInf, t1 = RL(0.0), t_surf = kInf;
-  uint32_t tpix = 0u;
-  int tsample = 0, tseg = 0;
-  for (;;) {
-    // ================================================ owner step
-    const unsigned long long rmask = wg_take_ready(Q, wave_in_block);
-    bool pub = false;
-    RayCtx Ro;  // the owner's ray: the segment just traced, then the next one
-    Ro.self_inst = -1;
-    if (ost == ST_WAIT && ((rmask >> wg_lane()) & 1ull)) {
-      Ro.o = mk3(Q.o[slot], Q.o[B + slot], Q.o[2 * B + slot]);
-      Ro.d = mk3(Q.d[slot], Q.d[B + slot], Q.d[2 * B + slot]);
-      Ro.time = kTime ? Q.time[slot] : RL(0.0);
-      Ro.self_gid = Q.self[slot];
-      f3 L = mk3(RL(0.), RL(0.), RL(0.));
-      if (shade<kTex, kMats, false>(P, prims, I.pix, I.sample, seg, Q.t[slot], Q.prim[slot],
-                                    kMedia ? Q.hitm[slot] : -1, Ro, L, T)) {
-        RT_HOOK_SAMPLE(I.pix, I.sample, L);
-        acc_sample(acc, L, bad);
-        ++I.sample;
-        ost = I.sample < I.s_end ? ST_NEED_SAMPLE : ST_NEED_ITEM;
-      } else {
-        pub = true;  // Ro is the next segment's ray
-      }
-    }
-    const bool need = ost == ST_NEED_ITEM;
-    work.commit(need && I.tp != -1, I.tp, acc, bad);
-    int aslot;
-    const int got = work.grab(need, aslot);
-    if (need) {
-      if (got >= P.n_items) {
-        ost = ST_DONE;
-        I.tp = -1;
-      } else {
-        acc_clear(acc);
-        bad = false;
-        ost = open_item<false>(P, got, I) ? ST_NEED_SAMPLE : ST_NEED_ITEM;
-        I.tp = work.tag(I.tp, aslot);
-      }
-    }
-    if (ost == ST_NEED_SAMPLE) {
-      camera_ray(P, I.pix, I.sample, ~0u, Ro);
-      T = mk3(RL(1.), RL(1.), RL(1.));
-      seg = 0;
-      pub = true;
-    }
-    if (pub) {
-      RT_COUNT(2);
-      Closest C0 = no_hit();
-      prefix_hits<false>(P, prims, Ro, kTmin, C0);
-      Q.o[slot] = Ro.o.x;
-      Q.o[B + slot] = Ro.o.y;
-      Q.o[2 * B + slot] = Ro.o.z;
-      Q.d[slot] = Ro.d.x;
-      Q.d[B + slot] = Ro.d.y;
-      Q.d[2 * B + slot] = Ro.d.z;
-      if constexpr (kTime) Q.time[slot] = Ro.time;
-      Q.self[slot] = Ro.self_gid;
-      Q.t[slot] = C0.t;
-#if RT_F64
-      Q.ord[slot] = C0.ord;
-#else
-      Q.ord[slot] = (int)(uint32_t)C0.key;
-#endif
-      Q.prim[slot] = C0.prim;
-      if constexpr (kMedia) {
-        Q.psx[slot] = I.pix;
-        Q.psx[B + slot] = (uint32_t)I.sample;
-        Q.psx[2 * B + slot] = (uint32_t)seg;
-      }
-      ost = ST_WAIT;
-    }
-    wg_push(Q, pub, slot);
-    // the wave is done once its paths are and it holds no one else's ray
-    if (RT_BALLOT_COUNT(ost != ST_DONE || tr) == 0) break;
-    // ================================================ tracer step
-    const int n_wait = RT_BALLOT_COUNT(ost == ST_WAIT);
-    bool idle = true;
-    for (;;) {
-      const int ps = wg_pop(Q, !tr);
-      if (ps >= 0) {
-        tr = true;
-        tslot = ps;
-        R.o = mk3(Q.o[ps], Q.o[B + ps], Q.o[2 * B + ps]);
-        R.d = mk3(Q.d[ps], Q.d[B + ps], Q.d[2 * B + ps]);
-        R.time = kTime ? Q.time[ps] : RL(0.0);
-        R.self_gid = Q.self[ps];
-        R.self_inst = -1;
-        prep_ray(R);
-        trav_begin(S, P.surface_root, kTmin);
-        S.C.t = Q.t[ps];
-        S.C.prim = Q.prim[ps];
-#if RT_F64
-        S.C.ord = Q.ord[ps];
-#else
-        S.C.key = hit_key(S.C.t, Q.ord[ps]);
-#endif
-        q = 0;
-        best = -1;
-        hit_medium = -1;
-        tbest = kInf;
-        if constexpr (kMedia) {
-          tpix = Q.psx[ps];
-          tsample = (int)Q.psx[B + ps];
-          tseg = (int)Q.psx[2 * B + ps];
-        }
-      }
-      if (RT_BALLOT_COUNT(tr) == 0) break;
-      // back to the owner step once enough of this wave's waiting paths have their results
-      const int n_ready = (int)__builtin_popcountll(wg_peek_ready(Q, wave_in_block));
-      if (n_ready > 0 && n_ready * 100 >= n_wait * P.trav_exit_pct) break;
-      idle = false;
-      if (tr) {
-        trav_round<false, kLeaf>(P, R, S, TW, overflow RT_PROF_NULLARG);
-        while (trav_done(S)) {
-          int next_m = -1;  // medium whose first query starts next
-          if (q == 0) {
-            tbest = t_surf = S.C.t;
-            best = S.C.prim;
-            next_m = 0;
-          } else {
-            const int m = (q - 1) >> 1;
-            next_m = m + 1;
-            if ((q & 1) == 1) {  // first boundary hit of medium m
-              if (S.C.prim >= 0) {
-                t1 = S.C.t;
-                if (prim_front(P, prims, S.C.prim, R, t1)) {
-                  if (t1 < tbest) {  // entering: the exit hit bounds the segment
-                    q = q + 1;
-                    trav_begin(S, P.media[m].root, t1);
-                    next_m = -1;
-                  }
-                } else {
-                  medium_event(P, m, tpix, tsample, tseg, kTmin, t1, tbest, hit_medium);
-                }
-              }
-            } else if (S.C.prim >= 0) {  // exit hit of medium m
-              medium_event(P, m, tpix, tsample, tseg, t1, S.C.t, tbest, hit_medium);
-            }
-          }
-          while (next_m >= 0 && next_m < n_media && P.media[next_m].alias_surface) {
-            if (best >= 0 && !prim_front(P, prims, best, R, t_surf))
-              medium_event(P, next_m, tpix, tsample, tseg, kTmin, t_surf, tbest, hit_medium);
-            ++next_m;
-          }
-          bool fin = false;
-          if (next_m >= 0) {
-            if (next_m < n_media) {
-              q = 1 + 2 * next_m;
-              trav_begin(S, P.media[next_m].root, kTmin);
-            } else {
-              fin = true;
-            }
-          }
-          if (fin) {  // the segment's queries are complete: its result to the owner
-            Q.t[tslot] = tbest;
-            Q.prim[tslot] = best;
-            if constexpr (kMedia) Q.hitm[tslot] = hit_medium;
-            wg_set_ready(Q, tslot);
-            tr = false;
-            break;
-          }
-          if (S.node != RT_EMPTY_ROOT) break;
-          if constexpr (kLeaf != 0)
-            test_leaf_generic<false>(P, R, S);
-          else
-            trav_round<false, kLeaf>(P, R, S, TW, overflow RT_PROF_NULLARG);
-        }
-      }
-    }
-#ifndef RT_HOST_EMU
-    if (idle && rmask == 0ull) __builtin_amdgcn_s_sleep(2);  // nothing to shade or trace: let the others run
-#else
-    (void)idle;
-#endif
-  }
   return overflow;
 }
 

@@ -41,16 +41,6 @@ int run_loop(const RT_NS::KernelParams& P, int variant, G& g, const RT_NS::Trav&
   unsigned long long words[6] = {0, 0, 0, 0, 0, 0};
   RT_NS::AccLds acc{words, 1};
   if (variant & RT_VAR_INST) return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, true, 0>(P, g, W, P.prims, acc);
-  if ((variant & RT_VAR_BASE) == RT_VAR_BVH_WG) {
-    // the workgroup ray queue with one lane per workgroup: the lane traces its own rays through it
-    std::vector<char> qmem(RT_NS::wg_queue_bytes(1, true, true) + 64, 0);
-    RT_NS::WgQueue Q = RT_NS::wg_queue_at(qmem.data(), 1, true, true);
-    for (int i = 0; i < RT_NS::kWgRing; ++i) Q.ring[i] = 0xffffffffu;
-    if (variant & RT_VAR_LEAF_TRI) return RT_NS::lane_loop_wg<kTex, kMedia, kMats, 1>(P, g, W, P.prims, acc, Q, 0, 0);
-    if ((variant & RT_VAR_LEAF_SPHERE) && !kMedia)
-      return RT_NS::lane_loop_wg<kTex, kMedia, kMats, 2>(P, g, W, P.prims, acc, Q, 0, 0);
-    return RT_NS::lane_loop_wg<kTex, kMedia, kMats, 0>(P, g, W, P.prims, acc, Q, 0, 0);
-  }
   if ((variant & RT_VAR_BASE) == RT_VAR_BVH) {  // one-class leaves, as the device kernels
     if (variant & RT_VAR_LEAF_TRI) return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, false, 1>(P, g, W, P.prims, acc);
     if ((variant & RT_VAR_LEAF_SPHERE) && !kMedia)
