@@ -12,7 +12,7 @@ for cfg in $CFGS; do
     nm=$(basename $lib .so); [ ${REPS:-1} -gt 1 ] && nm=${nm}_r$rep
     if [ "$lib" = base ]; then unset RT_AMD_LIB; else export RT_AMD_LIB=$PWD/$lib; fi
     timeout -k 10 200 python bench.py --no-cpu-baseline --no-f32 --precision ${PREC:-f64} --config $n --steps $STEPS --sim-shards $sh > $OUT/${n}_${sh}_$nm.json 2>>$OUT/err.log || { echo "$nm failed"; exit 1; }
-    python3 -c "import json;d=json.load(open('$OUT/${n}_${sh}_$nm.json'));print('$n shards $sh $nm', d['roofline']['kernel_ms'], d['ms_per_step'], d['check']['mean_rgb'])"
+    python3 -c "import json;d=json.load(open('$OUT/${n}_${sh}_$nm.json'));print('$n shards $sh $nm', d['roofline']['kernel_ms'], d['ms_per_step'], d['check']['sha16'])"
   done
   done
 done
