@@ -225,8 +225,6 @@ void fill_records(const rt_scene* sc, const std::vector<int>& order, const std::
     d.gid_code = codes[b].gid_code;
     d.prim_base = codes[b].prim_base;
     d.prim_code = codes[b].prim_code;
-    // axes along the world axes in order (exact zeros off the diagonal): rt_trace.h RT_BOX_ALIGNED
-    d.pad[0] = d.a0[1] == 0 && d.a0[2] == 0 && d.a1[0] == 0 && d.a1[2] == 0 && d.a2[0] == 0 && d.a2[1] == 0 ? 1 : 0;
     A.boxes.push_back(d);
   }
   A.prims.assign((size_t)n * 16, (R)0);

@@ -202,7 +202,7 @@ struct DevBoxT {
   int gid_code;
   int prim_base;   // primitive index of the faces
   int prim_code;
-  int pad[2];      // pad[0]: 1 = the axes are the world axes in order (rt_trace.h RT_BOX_ALIGNED)
+  int pad[2];
 };
 
 template <class R>

@@ -650,12 +650,7 @@ RT_FN int box_field(int base, int code, int f, bool& present) {
   present = off != RT_BOX_NO_FACE;
   return base + off;
 }
-// (RT_BOX_EXIT_SKIP=0: the exit face decoded for every lane, as in round 3).  RT_BOX_ALIGNED: a
-// binary64 box whose axes are the world axes in order (the Cornell room; rt_build.cpp marks it)
-// takes its six slab coordinates from one product each instead of a dot product
-#ifndef RT_BOX_ALIGNED
-#define RT_BOX_ALIGNED 1
-#endif
+// (RT_BOX_EXIT_SKIP=0: the exit face decoded for every lane, as in round 3)
 #ifndef RT_BOX_EXIT_SKIP
 #define RT_BOX_EXIT_SKIP 1
 #endif
@@ -682,24 +677,9 @@ RT_FN void test_box(const RT_CAS DevBox* B, const RayCtx& R, real tmin_up, Close
   // (d_i d_j) / (d_0 d_1 d_2) — one v_rcp_f64 and its correction instead of three (within ~4 ulp
   // of 1 / d_k).  A product that is zero, denormal or infinite (an axis parallel to the ray)
   // takes the three guarded reciprocals instead, a branch no lane normally enters.
-  real dk[3], invk[3], sk[3];
-#if RT_BOX_ALIGNED
-  if (B->pad[0]) {  // axis-aligned box (DevBox::pad[0], wave-uniform): its axes are e_k / L_k
-    dk[0] = ax[0].x * R.d.x;
-    dk[1] = ax[1].y * R.d.y;
-    dk[2] = ax[2].z * R.d.z;
-    sk[0] = ax[0].x * oc.x;
-    sk[1] = ax[1].y * oc.y;
-    sk[2] = ax[2].z * oc.z;
-  } else
-#endif
-  {
+  real dk[3], invk[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      dk[k] = dot(ax[k], R.d);
-      sk[k] = dot(ax[k], oc);
-    }
-  }
+  for (int k = 0; k < 3; ++k) dk[k] = dot(ax[k], R.d);
   {
     const real d01 = dk[0] * dk[1], p = d01 * dk[2];
     const real r = RT_RCP_NZ(p);
@@ -719,11 +699,7 @@ RT_FN void test_box(const RT_CAS DevBox* B, const RayCtx& R, real tmin_up, Close
 #else
     const real inv = RT_RCP(dot(ax[k], R.d));
 #endif
-#if RT_F64 && !defined(RT_BOX_THREE_RCP)
-    const real s = sk[k];
-#else
     const real s = dot(ax[k], oc);
-#endif
     const real t0 = -s * inv, t1 = RFMA(-s, inv, inv);  // the s = 0 and s = 1 planes
     // entering through the s = 1 end: t1 - t0 = inv, so t1 < t0 iff inv < 0 (the sign bit; the
     // two differ only when rounding makes t1 == t0, a slab |s| >= 2^52 box widths away)
