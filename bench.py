@@ -39,7 +39,11 @@ algorithmic bytes (the REFERENCE's traversal: every Cornell quad tested every se
 labelled `reference_traversal_bytes` figure — it exceeds HBM peak because the kernel reads its
 1.4 KB scene from the scalar cache, so it is never `frac`; `cpu_baseline` — the FP64 oracle, the
 CPU restatement of the reference's algorithm, on a bounded row sample, rank 0 at N=1 only, on
-every core this process may use (os.sched_getaffinity), with a 1-core figure beside it.
+every core this process may use (os.sched_getaffinity), with a 1-core figure beside it;
+`abi_device_list` — the drop-in's own multi-GPU path (what the Haskell binding calls): after the
+ranks' measurement rank 0 alone renders the frame through the C ABI's device list over GPUs
+0..N-1 (rt_multi_render, host-buffer output), ms per frame and the frame digest, which must equal
+the line's `check.sha16`.
 """
 import argparse
 import json
