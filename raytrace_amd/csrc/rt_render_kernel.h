@@ -81,6 +81,8 @@ struct WaveWork {
   unsigned long long* slots;
   int* hdr;
   unsigned free_mask;  // wave-uniform
+  // the kernel arguments re-read where used (rt_trace.h RT_KARGS): not held across the lane loop
+  __device__ __forceinline__ const KernelParams& kp() const { return RT_KARGS(P); }
 
   __device__ __forceinline__ WaveWork(const KernelParams& P_, int wave, int waves, unsigned long long* slots_)
       : P(P_), pool_base(wave * RT_POOL), pool_left(RT_POOL), offset(waves * RT_POOL), queue(wave & (RT_QUEUES - 1)),
@@ -97,11 +99,11 @@ struct WaveWork {
   // is flushed (so the commit path itself never waits on an LDS return or branches to a flush)
   __device__ __forceinline__ int open_pool(int b0, int cnt) {
     if (kSlots == 0 || cnt <= 0) return -1;
-    const bool big = b0 < P.big_items;
-    if (big ? (!P.agg_big || b0 + cnt > P.big_items) : !P.agg_small) return -1;
+    const bool big = b0 < kp().big_items;
+    if (big ? (!kp().agg_big || b0 + cnt > kp().big_items) : !kp().agg_small) return -1;
     if (free_mask == 0u) reclaim();
     if (free_mask == 0u) return -1;
-    const int tplo = (int)fast_div((uint32_t)(big ? b0 : b0 - P.big_items), big ? P.div_big : P.div_small);
+    const int tplo = (int)fast_div((uint32_t)(big ? b0 : b0 - kp().big_items), big ? kp().div_big : kp().div_small);
     const int s = __builtin_ctz(free_mask);
     free_mask &= free_mask - 1u;
     hdr[s] = cnt;  // every active lane stores the same words
@@ -136,7 +138,7 @@ struct WaveWork {
       return item;
     }
     // ranks [0, pool_left) drain the pool; the others are served by refills, in rank order
-    const int n_items = P.n_items;
+    const int n_items = kp().n_items;
     int item = rank < pool_left ? pool_base + rank : n_items;
     int first = pool_left, rest = cnt - pool_left;
     pool_left = 0;
@@ -147,7 +149,7 @@ struct WaveWork {
       const int qs = offset + queue * len;
       const int qlen = min(len, n_items - qs);  // <= 0 for an empty last queue
       int base = 0;
-      if (lane == leader) base = atomicAdd(P.counter + 64 * queue, RT_POOL);
+      if (lane == leader) base = atomicAdd(kp().counter + 64 * queue, RT_POOL);
       base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
       if (base >= qlen) {  // spent: ids are only ever handed out below qlen
         queue = (queue + 1) & (RT_QUEUES - 1);
@@ -176,7 +178,7 @@ struct WaveWork {
   // wave-collective: lanes with c add their finished item's fixed-point sums (rt_trace.h Acc:
   // [hi.xyz] or [hi.xyz, lo.xyz]; zero words are skipped) to its pool's slot, or to `accum`
   __device__ __forceinline__ void direct(int tp, const Acc& A) const {
-    unsigned long long* a = P.accum + RT_ACC_WORDS(real) * (size_t)tp;
+    unsigned long long* a = kp().accum + RT_ACC_WORDS(real) * (size_t)tp;
 #pragma unroll
     for (int c = 0; c < 3; ++c)
       if (A.hi[c]) atomicAdd(a + c, (unsigned long long)A.hi[c]);
@@ -187,10 +189,10 @@ struct WaveWork {
 #endif
   }
   // an item's tile pixel tagged with its slot code in bits 24-31 (rt_trace.h ItemCtx::tp): slot +
-  // 1, or 0 for direct commits.  The code exists only in launches that aggregate (P.agg_big |
-  // P.agg_small, set by the host for tiles below 2^24 pixels); elsewhere the word is the plain tile
+  // 1, or 0 for direct commits.  The code exists only in launches that aggregate (kp().agg_big |
+  // kp().agg_small, set by the host for tiles below 2^24 pixels); elsewhere the word is the plain tile
   // pixel, whose bits 24-30 may be set (tiles up to 2^31 pixels), and commit must not decode it
-  __device__ __forceinline__ bool aggregating() const { return kSlots > 0 && (P.agg_big | P.agg_small) != 0; }
+  __device__ __forceinline__ bool aggregating() const { return kSlots > 0 && (kp().agg_big | kp().agg_small) != 0; }
   __device__ __forceinline__ int tag(int tp, int slot) const {
     if (slot < 0) return tp;
     return tp | ((slot + 1) << 24);
@@ -216,7 +218,7 @@ struct WaveWork {
 #endif
       __hip_atomic_fetch_add(hdr + s, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // no return
     }
-    if (bad) atomicOr(P.nanflag + tp, 1u);
+    if (bad) atomicOr(kp().nanflag + tp, 1u);
   }
   // add a closed slot's words to `accum` (consecutive pixels: consecutive addresses) and free it
   __device__ __forceinline__ void flush(int s) {
@@ -226,13 +228,13 @@ struct WaveWork {
     const int r = (int)__popcll(act & ((1ull << __lane_id()) - 1ull));
     const int tplo = __builtin_amdgcn_readfirstlane(hdr[kSlots + s]);
     const long long g0 = (long long)tplo * RT_ACC_WORDS(real);
-    const long long g_end = (long long)P.tile_rows * P.cam.width * RT_ACC_WORDS(real);
+    const long long g_end = (long long)kp().tile_rows * kp().cam.width * RT_ACC_WORDS(real);
     unsigned long long* w = slots + s * kW;
     for (int j = r; j < kW; j += k) {
       const unsigned long long v = w[j];
       if (v != 0ull) {
         w[j] = 0ull;
-        if (g0 + j < g_end) atomicAdd(P.accum + g0 + j, v);
+        if (g0 + j < g_end) atomicAdd(kp().accum + g0 + j, v);
       }
     }
     free_mask |= 1u << s;
@@ -250,7 +252,8 @@ struct WaveWork {
 //    segment with the whole wave (kept for experiments; images are bit-identical).
 // Register budget: occupancy floor (waves per SIMD), per kernel class and precision — the table
 // below (RT_WAVES_OF): FP32 flat 7 (5 with noise textures), FP32 BVH 6 without media and constant
-// textures, else 5; binary64 flat 4 / 2, binary64 BVH 4, 3 with media.  Each entry was measured
+// textures, else 5; FP32 flat with constant textures 8; binary64 flat 5 (constant textures, the
+// diffuse materials) / 2, binary64 BVH 4, 3 with media.  Each entry was measured
 // against its neighbours.
 #ifndef RT_WAVES_FLAT
 #define RT_WAVES_FLAT 7
@@ -261,10 +264,13 @@ struct WaveWork {
 #ifndef RT_WAVES_BVH
 #define RT_WAVES_BVH 5
 #endif
-// knobs for the lightest instantiations (constant textures; BVH: no media): measured, 8 waves
-// for the Cornell kernel (62 VGPRs, 6 spilled) -0.3..0.7 %, 6 for the bunny's (80, 4 spilled) +3.4 %
+// knobs for the lightest instantiations (constant textures; BVH: no media).  The flat kernel with
+// constant textures runs 8 waves since round 4: with the kernel arguments re-read per iteration
+// (rt_trace.h RT_KARGS) and shade's unconditional ray update it needs 64 VGPRs without spills
+// (Cornell FP32 3.162 -> 3.075 ms against 7 waves, profiles/r4/unc_ab); round 3's 8-wave build
+// spilled 6 VGPRs and gained nothing
 #ifndef RT_WAVES_FLAT_TEX0
-#define RT_WAVES_FLAT_TEX0 7
+#define RT_WAVES_FLAT_TEX0 8
 #endif
 #ifndef RT_WAVES_BVH_LITE
 #define RT_WAVES_BVH_LITE 6  // 80 VGPRs once the item sums moved to LDS: bunny-Cornell 107.2 -> 100.6 ms at 6 (profiles/r3/slim)
@@ -273,7 +279,7 @@ struct WaveWork {
 // lightest instantiations (constant textures, no media, no materials beyond the diffuse ones)
 // keep more waves
 #ifndef RT_WAVES64_FLAT_LITE
-#define RT_WAVES64_FLAT_LITE 4
+#define RT_WAVES64_FLAT_LITE 5  // 96 VGPRs, no spills (round 4): Cornell binary64 5.442 -> 5.315 ms against 4
 #endif
 #ifndef RT_WAVES64_FLAT
 #define RT_WAVES64_FLAT 2  // readme f64 0.87 -> 0.78 ms at 2 (4: 1.31); the BVH kernels keep 3 (2: demo1 +23 %, pawn+fog +17 %)

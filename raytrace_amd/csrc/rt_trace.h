@@ -1284,6 +1284,29 @@ RT_FN_SPEC void closest<false>(const KernelParams& P, cfp prims, int root, int s
   C = S.C;
 }
 
+// The kernel arguments through a pointer the compiler cannot see through (RT_KARGS): a field read
+// after it is a scalar load from the kernarg segment at that point, not a value hoisted out of the
+// persistent lane loop and held in SGPRs for the whole kernel.  The lane loops re-derive P at
+// each phase (front end, traversal round, shading; the flat loop per iteration) and the work queue
+// per call (rt_render_kernel.h WaveWork::kp): the camera, material, target and queue fields are
+// then live for their phase only.  SGPR spills (each restore a v_readlane, a VALU instruction, in
+// the loop) 31 / 56 / 84 -> 0 / 2 / 2 in the binary64 Cornell / bunny / demo1 kernels, none left in
+// a loop; demo1 binary64 -4.2 %, pawn+fog -1.8 % (profiles/r4/kargs_ab).  The kernel's one
+// argument is its KernelParams, so the kernarg segment starts with it.
+#ifndef RT_KARGS_OPAQUE
+#define RT_KARGS_OPAQUE 1
+#endif
+#if defined(RT_HOST_EMU) || !RT_KARGS_OPAQUE
+#define RT_KARGS(P0) (P0)
+#else
+RT_FN const KernelParams& rt_kargs() {
+  const RT_CAS KernelParams* pp = (const RT_CAS KernelParams*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(pp));
+  return *(const KernelParams*)pp;
+}
+#define RT_KARGS(P0) rt_kargs()
+#endif
+
 // ------------------------------------------------------------------ per-path pieces
 // Ray.hs:157-172, 229: pixel jitter, time, defocus-disk point -> primary ray
 RT_FN uint32_t fast_div(uint32_t n, const FastDiv& f) {
@@ -1347,9 +1370,10 @@ RT_FN void medium_event(const KernelParams& P, int m, uint32_t pix, int sample, 
 // (and seg).  Returns true when the path terminates.
 // kMats: the scene has materials beyond lightSource / pitchBlack / lambertian; their code is
 // compiled only into those instantiations (the Cornell box and the bunny have none: -2.4 % / -1.2 %)
-template <int kTex, bool kMats, bool kInst = false>
-RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int& seg, real tbest, int best,
-                 int hit_medium, RayCtx& R, f3& L, f3& T, int best_inst = -1) {
+template <int kTex, bool kMats, bool kInst>
+RT_FN bool shade_event(const KernelParams& P, cfp prims, uint32_t pix, int sample, int seg, real tbest, int best,
+                       int hit_medium, const RayCtx& R, f3& L, const f3& T, int best_inst, f3& np, f3& nd, f3& Tf,
+                       int& ngid) {
   RT_HOOK_SEGMENT(pix, sample, seg, R, tbest, best, hit_medium, L, T);
   if (hit_medium < 0 && best < 0) {
     // miss: cs_background (Ray.hs:179)
@@ -1406,8 +1430,7 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
   f3 tex = f3{Mp->c0[0], Mp->c0[1], Mp->c0[2]};
   if (need_tex) tex = eval_texture<kTex == 2>(P, Mt.tex, h.u, h.v, h.p);
   u4 w = philox(pix, (uint32_t)sample, (uint32_t)seg, RT_EV_SCATTER, P.key0, P.key1);
-  const bool last = seg + 1 >= P.cam.max_depth;  // rayColor (depth - 1) with depth - 1 <= 0 is zero
-  f3 newdir = R.d;
+  f3 newdir;  // set where the path goes on (the caller reads it only there)
   switch (Mt.kind) {
     case 0:  // lightSource: emit, Absorb
       L = L + T * tex;
@@ -1417,15 +1440,21 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
       terminate = true;
       break;
     case 4:  // mirror
-      if constexpr (!kMats) break;
-      T = T * tex;
+      if constexpr (!kMats) {  // not in this scene (the host compiles these materials in when used)
+        terminate = true;
+        break;
+      }
+      Tf = tex;
       newdir = unit(reflect(h.n, R.d));
       break;
     case 5: {  // metal
-      if constexpr (!kMats) break;
+      if constexpr (!kMats) {  // not in this scene (the host compiles these materials in when used)
+        terminate = true;
+        break;
+      }
       f3 d2 = reflect(h.n, R.d) + Mt.param * unit_vector(w.y, w.z);
       if (dot(d2, h.n) > RL(0.0)) {
-        T = T * tex;
+        Tf = tex;
         newdir = normalize(d2);
       } else {
         terminate = true;
@@ -1433,7 +1462,11 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
       break;
     }
     case 6: {  // dielectric
-      if constexpr (!kMats) break;
+      if constexpr (!kMats) {  // not in this scene (the host compiles these materials in when used)
+        terminate = true;
+        break;
+      }
+      Tf = mk3(RL(1.), RL(1.), RL(1.));
       real ior = Mt.param;
       real ratio = h.front ? RT_RCP(ior) : ior;
       real cos_t = RMIN(RL(1.0), -dot(h.n, R.d));
@@ -1451,8 +1484,12 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
       break;
     }
     case 7:  // transparent
-      if constexpr (!kMats) break;
-      T = T * tex;
+      if constexpr (!kMats) {  // not in this scene (the host compiles these materials in when used)
+        terminate = true;
+        break;
+      }
+      Tf = tex;
+      newdir = R.d;
       break;
     default: {  // 2 lambertian, 3 lommelSeeliger (HemisphereF); 8 isotropic, 9 anisotropic (SphereF)
       const bool hemi = !kMats || Mt.kind == 2 || Mt.kind == 3;
@@ -1496,23 +1533,43 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
         real base = RL(1.0) + g * g - RL(2.0) * g * mu;
         f = ((RL(1.0) - g * g) * RT_RCP(base * RT_SQRT(base))) * f;
       }
-      T = T * ((pdf1 * RT_RCP(pdf)) * f);
+      Tf = (pdf1 * RT_RCP(pdf)) * f;
       newdir = dir;
       break;
     }
   }
-  if (!terminate) {
-    if (last) {
-      terminate = true;
-    } else {
-      R.o = h.p;
-      R.d = newdir;
-      R.self_gid = h.gid;
-      if constexpr (kInst) R.self_inst = hit_medium >= 0 ? -1 : best_inst;
-      ++seg;
-    }
-  }
+  np = h.p;
+  nd = newdir;
+  ngid = h.gid;
   return terminate;
+}
+// One rayColor level (shade_event) and the path's next segment.  The next origin, direction,
+// throughput factor and self id are defined only where the path goes on (no exit of shade_event
+// carries the unchanged ray to a join), and the loop-carried ray and throughput are written
+// unconditionally: a path that ends is restarted by camera_ray (origin, direction, self ids) with
+// a fresh throughput and segment count before anything reads them.  In the flat binary64 kernel
+// the joins' copies were ~40 v_mov per lane-loop iteration, and selects in their place ~20.
+template <int kTex, bool kMats, bool kInst = false>
+RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int& seg, real tbest, int best,
+                 int hit_medium, RayCtx& R, f3& L, f3& T, int best_inst = -1) {
+#ifdef RT_HOST_EMU
+  f3 np = R.o, nd = R.d, Tf = mk3(RL(1.), RL(1.), RL(1.));  // (defined on the CPU too)
+  int ngid = R.self_gid;
+#else
+  f3 np, nd, Tf;
+  int ngid;
+#endif
+  const bool term =
+      shade_event<kTex, kMats, kInst>(P, prims, pix, sample, seg, tbest, best, hit_medium, R, L, T, best_inst, np, nd, Tf, ngid);
+  R.o = np;
+  R.d = nd;
+  T = T * Tf;
+  R.self_gid = ngid;
+  if constexpr (kInst) R.self_inst = hit_medium >= 0 ? -1 : best_inst;
+  // rayColor (depth - 1) with depth - 1 <= 0 is zero: the path ends at the last depth (Ray.hs:176)
+  const bool cont = !term && seg + 1 < P.cam.max_depth;
+  ++seg;
+  return !cont;
 }
 
 // Work item -> pixel / sample range.  Ids are pixel-major within each item size (rt_internal.h
@@ -1559,7 +1616,7 @@ RT_FN bool open_item(const KernelParams& P, int item, ItemCtx& I) {
 // kernel (every lane tests the same primitives), and the lockstep BVH variant kept for
 // experiments (RT_VAR_BVH_LOCKSTEP; BVH scenes, media or not, default to lane_loop_bvh).
 template <bool kFlat, int kTex, bool kMedia, bool kMats, class Work, class AccT>
-RT_FN int lane_loop_lockstep(const KernelParams& P, Work& work, const Trav& TW, const real* prims_, AccT& acc) {
+RT_FN int lane_loop_lockstep(const KernelParams& P0, Work& work, const Trav& TW, const real* prims_, AccT& acc) {
   const cfp prims = cf(prims_);
   int overflow = 0;
   ItemCtx I{-1, 0, 0, 0u, 0u};
@@ -1579,6 +1636,7 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Work& work, const Trav& TW, 
   R.self_gid = -1;
   R.self_inst = -1;
   for (;;) {
+    const KernelParams& P = RT_KARGS(P0);  // (per iteration: RT_KARGS)
     const bool need = !alive && I.sample >= I.s_end;
     work.commit(need && I.tp != -1, I.tp, acc, bad);
     int aslot;
@@ -1656,9 +1714,9 @@ RT_FN int lane_loop_lockstep(const KernelParams& P, Work& work, const Trav& TW, 
 // soon as the previous one finishes.
 enum : int { ST_NEED_ITEM = 0, ST_NEED_SAMPLE = 1, ST_START_SEG = 2, ST_TRACE = 3, ST_SHADE = 4 };
 template <int kTex, bool kMedia, bool kMats, bool kInst, int kLeaf, class Work, class AccT>
-RT_FN int lane_loop_bvh(const KernelParams& P, Work& work, const Trav& TW, const real* prims_, AccT& acc) {
+RT_FN int lane_loop_bvh(const KernelParams& P0, Work& work, const Trav& TW, const real* prims_, AccT& acc) {
   const cfp prims = cf(prims_);
-  const int n_media = kMedia ? P.n_media : 0;  // media code only in the kMedia instantiations
+  const int n_media = kMedia ? P0.n_media : 0;  // media code only in the kMedia instantiations
   int overflow = 0;
   ItemCtx I{-1, 0, 0, 0u, 0u};
   int seg = 0;
@@ -1686,6 +1744,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Work& work, const Trav& TW, const
   real tbest = kInf, t1 = RL(0.0), t_surf = kInf;
   RT_PROF_DECL
   for (;;) {
+    const KernelParams& P = RT_KARGS(P0);  // (per phase: RT_KARGS)
     // ---- front end: items, samples, segment starts (lanes not tracing)
     const bool need = state == ST_NEED_ITEM;
     RT_PROF_ADD(PF_ITERS, 1);
@@ -1721,6 +1780,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Work& work, const Trav& TW, const
     RT_PROF_MARK(PF_FRONT);
     // ---- traversal rounds; a finished query starts the segment's next one in place
     for (;;) {
+      const KernelParams& P = RT_KARGS(P0);
       const bool tr = state == ST_TRACE;
       const int n_tr = RT_BALLOT_COUNT(tr);
       if (n_tr == 0) break;
@@ -1787,6 +1847,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P, Work& work, const Trav& TW, const
     RT_PROF_ADD(PF_SHADING, RT_BALLOT_COUNT(state == ST_SHADE));
     // ---- shade the segments whose queries are complete
     if (state == ST_SHADE) {
+      const KernelParams& P = RT_KARGS(P0);
       f3 L = mk3(RL(0.), RL(0.), RL(0.));
       if (shade<kTex, kMats, kInst>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T, best_inst)) {
         RT_HOOK_SAMPLE(I.pix, I.sample, L);
