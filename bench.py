@@ -42,8 +42,8 @@ CPU restatement of the reference's algorithm, on a bounded row sample, rank 0 at
 every core this process may use (os.sched_getaffinity), with a 1-core figure beside it;
 `abi_device_list` — the drop-in's own multi-GPU path (what the Haskell binding calls): after the
 ranks' measurement rank 0 alone renders the frame through the C ABI's device list over GPUs
-0..N-1 (rt_multi_render, host-buffer output), ms per frame and the frame digest, which must equal
-the line's `check.sha16`.
+0..N-1 (rt_multi_render, host-buffer output) once the other ranks have exited, ms per frame and
+the frame digest, which must equal the line's `check.sha16`.
 """
 import argparse
 import json
@@ -206,8 +206,7 @@ def abi_device_list(world, cs, seed, devices, precision, frames, warmup=2, warmu
     m = MultiDeviceScene(world, devices)
     try:
         tw, k = time.perf_counter(), 0
-        # uploads, occupancy queries, the resident buffers; then at least warmup_s of frames (the
-        # ranks that just left the process group may still be tearing down on these devices)
+        # uploads, occupancy queries, the resident buffers; then at least warmup_s of frames
         while k < warmup or time.perf_counter() - tw < warmup_s:
             m.render(cs, seed, precision=precision, row_block=1)
             k += 1
@@ -228,6 +227,23 @@ def abi_device_list(world, cs, seed, devices, precision, frames, warmup=2, warmu
             "device_allocs_timed": allocs,
             "sha16": hashlib.sha256(np.ascontiguousarray(img).tobytes()).hexdigest()[:16],
             "note": "one process, rt_multi_render over the device list (C-ABI drop-in path), host-buffer output"}
+
+
+def wait_exited(pids, timeout_s=120.0):
+    """Wait until the processes `pids` have exited (gone, or zombies whose GPU contexts are already
+    released); returns the seconds waited.  Gives up after timeout_s (the record then carries it)."""
+    t0 = time.perf_counter()
+
+    def alive(pid):
+        try:
+            with open(f"/proc/{pid}/stat") as f:
+                return f.read().rsplit(")", 1)[1].split()[0] != "Z"
+        except OSError:
+            return False
+
+    while any(alive(p) for p in pids) and time.perf_counter() - t0 < timeout_s:
+        time.sleep(0.05)
+    return time.perf_counter() - t0
 
 
 def spawn_ranks(n):
@@ -488,18 +504,26 @@ def main():
             _, f32 = record("f32")
             f32["note"] = "FP32 fast path (rt_exec.flags RT_EXEC_F32), same frames, measured after the f64 line"
             line["f32_fast_path"] = f32
+    others = []
     if n > 1:
+        pids = [None] * n
+        dist.all_gather_object(pids, os.getpid())
+        others = [p for r, p in enumerate(pids) if r != rank]
         dist.barrier()
         dist.destroy_process_group()
     scene.close()
     if rank == 0:
-        # the drop-in's own multi-GPU path over the same N GPUs, after the ranks' measurement (the
-        # process group is gone): rank 0 alone drives every device through the C-ABI device list
+        # the drop-in's own multi-GPU path over the same N GPUs, after the ranks' measurement: rank 0
+        # alone drives every device through the C-ABI device list once the other ranks have EXITED —
+        # a second process holding a context on a GPU (even an idle one) slows the kernels there
+        # (one-GPU rehearsal: [0, 0] 13.9 ms per frame beside the idle ranks, 7.05 alone)
         if not args.no_abi_devices and n_sh == n:
             devs = [0] * n if one_device else list(range(n))
             try:
+                waited = wait_exited(others, timeout_s=120.0)
                 line["abi_device_list"] = abi_device_list(world, cs, seed, devs, precisions[0],
                                                           frames=max(args.steps, 5))
+                line["abi_device_list"]["waited_for_ranks_s"] = round(waited, 2)
                 line["abi_device_list"]["sha16_equals_line"] = (
                     main_rec["check"] is not None and line["abi_device_list"]["sha16"] == main_rec["check"]["sha16"])
             except Exception as e:  # never break the bench line

@@ -63,7 +63,14 @@ struct AggGeom {
   static constexpr int kWaveBytes = kSlots * kWords * 8 + 2 * kSlots * 4;
 };
 
-template <int kSlots, int kPix>
+// The work queue of the flat kernels re-reads its kernel-argument fields at each use; the BVH
+// kernels' does in FP32 only (binary64 demo1 / pawn+fog -0.7 % with them held, Cornell's flat
+// binary64 kernel +0.7 %: profiles/r4/kargs_phase_ab, r4/pp_ab)
+#ifndef RT_KARGS_WORK_BVH
+#define RT_KARGS_WORK_BVH (!RT_F64)
+#endif
+// kReread: the queue's kernel-argument fields re-read at each use (rt_trace.h RT_KARGS) or held
+template <int kSlots, int kPix, bool kReread>
 struct WaveWork {
   const KernelParams& P;
   // item claims: a pool of consecutive ids in SGPRs (wave-uniform state), refilled with ONE
@@ -82,7 +89,7 @@ struct WaveWork {
   int* hdr;
   unsigned free_mask;  // wave-uniform
   // the kernel arguments re-read where used (rt_trace.h RT_KARGS): not held across the lane loop
-  __device__ __forceinline__ const KernelParams& kp() const { return RT_KARGS(P); }
+  __device__ __forceinline__ const KernelParams& kp() const { return RT_KARGS_IF(kReread, P); }
 
   __device__ __forceinline__ WaveWork(const KernelParams& P_, int wave, int waves, unsigned long long* slots_)
       : P(P_), pool_base(wave * RT_POOL), pool_left(RT_POOL), offset(waves * RT_POOL), queue(wave & (RT_QUEUES - 1)),
@@ -348,7 +355,7 @@ void rt_render_kernel(KernelParams P) {
   smem_rest += kAggBytes / 4 * (int)(blockDim.x / 64);
   for (int i = (int)__lane_id(); i < kAggBytes / 8; i += 64) agg[i] = 0ull;
   if constexpr (kVar == RT_VAR_FLAT) {
-    WaveWork<kSlots, kPix> work(P, wave, waves, agg);
+    WaveWork<kSlots, kPix, true> work(P, wave, waves, agg);
     overflow = lane_loop_lockstep<true, kTex, kMedia, kMats>(P, work, Trav{nullptr, 0, nullptr}, P.prims, acc);
     work.finish();
   } else {
@@ -359,7 +366,7 @@ void rt_render_kernel(KernelParams P) {
       lds_nodes[i] = v4f{q.x, q.y, q.z, q.w};
     }
     __syncthreads();
-    WaveWork<kSlots, kPix> work(P, wave, waves, agg);
+    WaveWork<kSlots, kPix, RT_KARGS_WORK_BVH> work(P, wave, waves, agg);
     const Trav W{smem_rest + threadIdx.x, kBlock, lds_nodes};
     if constexpr (kVar == RT_VAR_BVH_LOCKSTEP)
       overflow = lane_loop_lockstep<false, kTex, kMedia, kMats>(P, work, W, P.prims, acc);

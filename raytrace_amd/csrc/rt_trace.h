@@ -1306,6 +1306,15 @@ RT_FN const KernelParams& rt_kargs() {
 }
 #define RT_KARGS(P0) rt_kargs()
 #endif
+// per-phase switches (1: re-read), measured per precision (profiles/r4/kargs_phase_ab): the FP32
+// BVH kernels keep the traversal rounds' arguments in SGPRs (bunny-Cornell / demo1 / pawn+fog
+// -0.9 / -0.9 / -1.0 % against re-reading them per round), the binary64 ones re-read them (pawn+fog
+// +0.7 % without); the BVH kernels' work queue re-reads its fields in FP32 only
+// (rt_render_kernel.h RT_KARGS_WORK_BVH)
+#ifndef RT_KARGS_TRAV
+#define RT_KARGS_TRAV RT_F64
+#endif
+#define RT_KARGS_IF(on, P0) ((on) ? RT_KARGS(P0) : (P0))
 
 // ------------------------------------------------------------------ per-path pieces
 // Ray.hs:157-172, 229: pixel jitter, time, defocus-disk point -> primary ray
@@ -1780,7 +1789,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P0, Work& work, const Trav& TW, cons
     RT_PROF_MARK(PF_FRONT);
     // ---- traversal rounds; a finished query starts the segment's next one in place
     for (;;) {
-      const KernelParams& P = RT_KARGS(P0);
+      const KernelParams& P = RT_KARGS_IF(RT_KARGS_TRAV, P0);
       const bool tr = state == ST_TRACE;
       const int n_tr = RT_BALLOT_COUNT(tr);
       if (n_tr == 0) break;
