@@ -18,7 +18,9 @@
 #   phase      phase profile (needs raytrace_amd/_lib/exp/librt_amd_prof.so, -DRT_PHASE_PROF)
 #   microbench VALU rate / binary64 math microbenchmarks, built from source here
 #   rehearse   bench.py --gpus 2 / 3 on one GPU, frames bit-identical to N = 1
+#   shards     tools/shard_share_sweep.sh: one rank's share of an N-GPU frame, N = 1, 2, 4, 8
 #   abiprobe   tools/abi_probe.py: the C-ABI device lists [0] x 1..3 in a process of their own
+#   abiprobe2  tools/abi_probe2.py: [0, 0] after torch / distributed set-up / under torchrun
 #   demo2fit   tools/demo2_fit.py: demo2 at 800 x 800 against the published demo2.png (depth sweep,
 #              renders for the spp estimate)
 # Env: CONFIGS, PRECS, CPS, AB_CFGS, REPS, PROF_STEPS, PYTEST_K, ROUND.  Each GPU step runs under
@@ -104,9 +106,19 @@ PY
       timeout -k 10 120 tools/microbench/f64_math_check > "$OUT/f64_math_check.json" || exit 1 ;;
     rehearse)
       bash tools/rehearse_dist.sh "$TAG/rehearse" || exit 1 ;;
+    shards)
+      bash tools/shard_share_sweep.sh "$TAG/shards" > "$OUT/shards.log" 2>&1 || { echo "shard sweep failed"; tail -5 "$OUT/shards.log"; exit 1; }
+      cat "$OUT/shards.log" ;;
     abiprobe)
       timeout -k 10 300 python3 -u tools/abi_probe.py ${ABI_CFG:-cornell} 20 > "$OUT/abi_probe.jsonl" 2> "$OUT/abi_probe.err" || { echo "abi_probe failed"; tail -20 "$OUT/abi_probe.err"; exit 1; }
       python3 -c "import json,sys; [print(d['devices'], d['ms_per_frame'], d['kernel_ms_max_device'], d['sha16'], d['calls'][-1]) for d in map(json.loads, open(sys.argv[1]))]" "$OUT/abi_probe.jsonl" ;;
+    abiprobe2)
+      for m in plain torch torch_tensors dist; do
+        timeout -k 10 200 python3 -u tools/abi_probe2.py $m >> "$OUT/abi_probe2.jsonl" 2>> "$OUT/abi_probe2.err" || { echo "abi_probe2 $m failed"; tail -5 "$OUT/abi_probe2.err"; exit 1; }
+      done
+      timeout -k 10 200 python3 -m torch.distributed.run --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29541 tools/abi_probe2.py plain \
+        | sed 's/"plain"/"torchrun_plain"/' >> "$OUT/abi_probe2.jsonl" 2>> "$OUT/abi_probe2.err" || { echo "abi_probe2 torchrun failed"; tail -5 "$OUT/abi_probe2.err"; exit 1; }
+      cat "$OUT/abi_probe2.jsonl" ;;
     demo2fit)
       timeout -k 10 600 python3 -u tools/demo2_fit.py "$OUT/demo2_fit.jsonl" > "$OUT/demo2_fit.log" 2>&1 || { echo "demo2_fit failed"; tail -20 "$OUT/demo2_fit.log"; exit 1; } ;;
     *)
