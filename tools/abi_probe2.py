@@ -1,6 +1,6 @@
 """Why the C-ABI device list is slower inside bench.py's N>1 rehearsal than alone (tools/abi_probe.py):
 the list [0, 0] timed after each of the things bench.py's rank 0 has done by then.
-usage: python tools/abi_probe2.py <mode>   mode: plain | torch | torch_tensors | dist
+usage: python tools/abi_probe2.py <mode>   mode: plain | torch | torch_tensors | dist | streams
 (one mode per process; tools/gpu_round.sh step `abiprobe2` runs them all)"""
 import json
 import os
@@ -16,6 +16,12 @@ if __name__ == "__main__":
     if mode != "plain":
         import torch
         torch.cuda.set_device(0)
+        if mode == "streams":  # bench.py's rank 0 has created streams of its own by then
+            ss = [torch.cuda.Stream() for _ in range(3)]
+            for st in ss:
+                with torch.cuda.stream(st):
+                    torch.ones(16, device="cuda:0").sum()
+            torch.cuda.synchronize()
         if mode in ("torch_tensors", "dist"):
             x = [torch.empty((600, 600, 3), dtype=torch.float64, device="cuda:0") for _ in range(4)]
             torch.cuda.synchronize()

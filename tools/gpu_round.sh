@@ -113,7 +113,7 @@ PY
       timeout -k 10 300 python3 -u tools/abi_probe.py ${ABI_CFG:-cornell} 20 > "$OUT/abi_probe.jsonl" 2> "$OUT/abi_probe.err" || { echo "abi_probe failed"; tail -20 "$OUT/abi_probe.err"; exit 1; }
       python3 -c "import json,sys; [print(d['devices'], d['ms_per_frame'], d['kernel_ms_max_device'], d['sha16'], d['calls'][-1]) for d in map(json.loads, open(sys.argv[1]))]" "$OUT/abi_probe.jsonl" ;;
     abiprobe2)
-      for m in plain torch torch_tensors dist; do
+      for m in ${ABI_MODES:-plain torch torch_tensors dist}; do
         timeout -k 10 200 python3 -u tools/abi_probe2.py $m >> "$OUT/abi_probe2.jsonl" 2>> "$OUT/abi_probe2.err" || { echo "abi_probe2 $m failed"; tail -5 "$OUT/abi_probe2.err"; exit 1; }
       done
       timeout -k 10 200 python3 -m torch.distributed.run --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29541 tools/abi_probe2.py plain \
