@@ -519,6 +519,8 @@ def main():
         # (one-GPU rehearsal: [0, 0] 13.9 ms per frame beside the idle ranks, 7.05 alone)
         if not args.no_abi_devices and n_sh == n:
             devs = [0] * n if one_device else list(range(n))
+            if os.environ.get("RT_BENCH_ABI_DEVICES"):  # diagnostic: another device list (e.g. "0,0")
+                devs = [int(x) for x in os.environ["RT_BENCH_ABI_DEVICES"].split(",")]
             try:
                 waited = wait_exited(others, timeout_s=120.0)
                 line["abi_device_list"] = abi_device_list(world, cs, seed, devs, precisions[0],

@@ -23,7 +23,13 @@
 #include <vector>
 
 #ifndef RT_BLOCK
-#define RT_BLOCK 256          // flat kernel workgroup
+// flat kernel workgroup: one wave.  Every wave has its own item pool and aggregation slots (nothing
+// is shared across a workgroup), so a finished wave frees its slot at once and the next launch's
+// waves (the other stream's frame) fill it; with 4-wave workgroups a slot waited for the
+// workgroup's slowest wave: Cornell binary64 5.161 -> 5.070 ms, one rank's share of 8 GPUs 0.747 ->
+// 0.728 ms, README's share of 8 -6 % (profiles/r4/wg_ab; round 3 measured 64 vs 256 within noise
+// at 1 GPU, before the kernels fit 5 / 8 waves per SIMD)
+#define RT_BLOCK 64
 #endif
 #ifndef RT_BLOCK_BVH
 #define RT_BLOCK_BVH 256      // BVH kernel workgroup at 5 waves/SIMD (others: rt_render_kernel.h RT_BLOCK_OF)
