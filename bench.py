@@ -284,7 +284,7 @@ def main():
                     help="the kernel precision of the line's value (f64: the reference's binary64)")
     ap.add_argument("--no-f32", action="store_true", help="skip the FP32 fast-path record after an f64 line")
     ap.add_argument("--check", action="store_true", help="gather + assemble + sanity-check the frame after timing")
-    ap.add_argument("--streams", type=int, default=0, choices=[0, 1, 2],
+    ap.add_argument("--streams", type=int, default=0, choices=[0, 1, 2, 3, 4],
                     help="frames alternate between this many HIP streams (2: frame i+1 fills the CUs that "
                          "frame i's last long paths leave idle); 0 = auto: 2 for flat scenes, 1 for BVH "
                          "scenes (two LDS-staging BVH launches interfere: bunny 20.7 -> 22.4 ms per frame)")
@@ -353,7 +353,7 @@ def main():
         # before reusing it).  Two streams at N > 1 take three buffers: gather i starts only after
         # frame i's resolve, which queues behind frame i+1's persistent grid, so with two
         # buffers frame i+2 would wait for that gather and leave frame i+1's tail alone on the CUs
-        nbuf = (3 if args.streams > 1 else 2) if n > 1 else (2 if args.streams > 1 else 1)
+        nbuf = args.streams + (1 if n > 1 and args.streams > 1 else 0) + (1 if n > 1 and args.streams == 1 else 0)
         tiles = [torch.empty((rows, w, 3), dtype=dtype, device=dev) for _ in range(nbuf)]
         gathered = [torch.empty((n * rows, w, 3), dtype=dtype, device=dev) for _ in range(nbuf)] if n > 1 else None
         works = [None] * nbuf
