@@ -210,12 +210,13 @@ def abi_device_list(world, cs, seed, devices, precision, frames, warmup=2, warmu
         while k < warmup or time.perf_counter() - tw < warmup_s:
             m.render(cs, seed, precision=precision, row_block=1)
             k += 1
-        kms, allocs = [], 0
+        kms, tms, allocs = [], [], 0
         t0 = time.perf_counter()
         for _ in range(frames):
             st = {}
             img = m.render(cs, seed, precision=precision, row_block=1, stats=st)
             kms.append(st["kernel_ms"])
+            tms.append(st["total_ms"])
             allocs += st["device_allocs"]
         dt = time.perf_counter() - t0
     finally:
@@ -224,6 +225,7 @@ def abi_device_list(world, cs, seed, devices, precision, frames, warmup=2, warmu
     return {"devices": list(devices), "dtype": precision, "frames": frames,
             "ms_per_frame": round(dt / frames * 1e3, 4), "value": round(samples * frames / dt / 1e6, 2),
             "unit": "Msamples/s", "kernel_ms_max_device": round(sum(kms) / len(kms), 4),
+            "library_ms_per_call": round(sum(tms) / len(tms), 4),  # rt_stats.total_ms: inside the C ABI
             "device_allocs_timed": allocs,
             "sha16": hashlib.sha256(np.ascontiguousarray(img).tobytes()).hexdigest()[:16],
             "note": "one process, rt_multi_render over the device list (C-ABI drop-in path), host-buffer output"}
