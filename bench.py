@@ -231,6 +231,20 @@ def abi_device_list(world, cs, seed, devices, precision, frames, warmup=2, warmu
             "note": "one process, rt_multi_render over the device list (C-ABI drop-in path), host-buffer output"}
 
 
+def abi_helper(args):
+    """--abi-helper: build the scene on the CPU, wait for 'go <d0,d1,...>' on stdin (rank 0 sends it
+    once the other ranks have exited), time the C-ABI device list over those devices in THIS process
+    and print its record as one JSON line.  Never touches a GPU before the go."""
+    from raytrace_amd import scenes
+    cs, world, seed = scenes.CONFIGS[args.config]()
+    cmd = sys.stdin.readline().split()
+    if len(cmd) != 2 or cmd[0] != "go":
+        return 0  # rank 0 ended without a measurement
+    devs = [int(x) for x in cmd[1].split(",")]
+    print(json.dumps(abi_device_list(world, cs, seed, devs, args.precision, frames=args.steps)), flush=True)
+    return 0
+
+
 def wait_exited(pids, timeout_s=120.0):
     """Wait until the processes `pids` have exited (gone, or zombies whose GPU contexts are already
     released); returns the seconds waited.  Gives up after timeout_s (the record then carries it)."""
@@ -297,11 +311,16 @@ def main():
                     help="diagnostic, one process: render only shard 0 of N (one rank's share of an N-GPU frame)")
     ap.add_argument("--no-abi-devices", action="store_true",
                     help="skip the abi_device_list record (rank 0, after the ranks' measurement)")
+    ap.add_argument("--abi-helper", action="store_true",
+                    help="internal: the process that times the C-ABI device list for rank 0 (started "
+                         "before rank 0 touches a GPU; waits for 'go <devices>' on stdin)")
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="nccl (= RCCL, the real path); gloo gathers through host memory (N>1 rehearsal on one "
                          "GPU, with RT_BENCH_ONE_DEVICE=1 mapping every rank to device 0); auto: gloo with "
                          "RT_BENCH_ONE_DEVICE=1, else nccl")
     args = ap.parse_args()
+    if args.abi_helper:
+        return abi_helper(args)
     if args.gpus < 1:
         raise SystemExit("bench.py: --gpus must be >= 1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -315,6 +334,17 @@ def main():
     if args.dist_backend == "auto":
         # RCCL refuses two ranks on one GPU: the one-device rehearsal gathers through gloo
         args.dist_backend = "gloo" if one_device else "nccl"
+
+    # N > 1: rank 0 starts the device-list process now, before this process touches a GPU (it is
+    # forked from a process without GPU state), and hands it the devices once the other ranks have
+    # exited: the drop-in's caller is a plain process of its own (no torch, no process group)
+    helper = None
+    if world_size > 1 and int(os.environ.get("RANK", "0")) == 0 and not args.no_abi_devices and args.sim_shards == 1:
+        import subprocess
+        henv = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+        helper = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--abi-helper", "--config", args.config,
+                                   "--precision", args.precision, "--steps", str(max(args.steps, 5))],
+                                  stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=henv)
 
     import torch
     import torch.distributed as dist
@@ -525,14 +555,23 @@ def main():
                 devs = [int(x) for x in os.environ["RT_BENCH_ABI_DEVICES"].split(",")]
             try:
                 waited = wait_exited(others, timeout_s=120.0)
-                line["abi_device_list"] = abi_device_list(world, cs, seed, devs, precisions[0],
-                                                          frames=max(args.steps, 5))
+                if helper is not None:
+                    out, _ = helper.communicate("go " + ",".join(map(str, devs)) + "\n", timeout=900)
+                    helper = None
+                    line["abi_device_list"] = json.loads(out.strip().splitlines()[-1])
+                    line["abi_device_list"]["process"] = "its own (started by rank 0 before any GPU call)"
+                else:
+                    line["abi_device_list"] = abi_device_list(world, cs, seed, devs, precisions[0],
+                                                              frames=max(args.steps, 5))
                 line["abi_device_list"]["waited_for_ranks_s"] = round(waited, 2)
                 line["abi_device_list"]["sha16_equals_line"] = (
                     main_rec["check"] is not None and line["abi_device_list"]["sha16"] == main_rec["check"]["sha16"])
             except Exception as e:  # never break the bench line
                 line["abi_device_list"] = {"error": repr(e)}
         print(json.dumps(line), flush=True)
+    if helper is not None:  # not used (an error above): let it go
+        helper.kill()
+        helper.wait()
 
 
 if __name__ == "__main__":
