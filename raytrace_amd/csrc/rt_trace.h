@@ -1292,7 +1292,9 @@ RT_FN_SPEC void closest<false>(const KernelParams& P, cfp prims, int root, int s
 // then live for their phase only.  SGPR spills (each restore a v_readlane, a VALU instruction, in
 // the loop) 31 / 56 / 84 -> 0 / 2 / 2 in the binary64 Cornell / bunny / demo1 kernels, none left in
 // a loop; demo1 binary64 -4.2 %, pawn+fog -1.8 % (profiles/r4/kargs_ab).  The kernel's one
-// argument is its KernelParams, so the kernarg segment starts with it.
+// argument is its KernelParams, so the kernarg segment starts with it: RT_KARGS(P0) stands for the
+// KERNEL'S OWN argument (never a modified copy — the kernels pass theirs, unmodified, to the lane
+// loops); the host emulator returns P0 itself.
 #ifndef RT_KARGS_OPAQUE
 #define RT_KARGS_OPAQUE 1
 #endif
