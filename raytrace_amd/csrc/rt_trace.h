@@ -1441,7 +1441,11 @@ RT_FN bool shade_event(const KernelParams& P, cfp prims, uint32_t pix, int sampl
   f3 tex = f3{Mp->c0[0], Mp->c0[1], Mp->c0[2]};
   if (need_tex) tex = eval_texture<kTex == 2>(P, Mt.tex, h.u, h.v, h.p);
   u4 w = philox(pix, (uint32_t)sample, (uint32_t)seg, RT_EV_SCATTER, P.key0, P.key1);
+#ifdef RT_HOST_EMU
+  f3 newdir = R.d;  // (defined on every path on the CPU)
+#else
   f3 newdir;  // set where the path goes on (the caller reads it only there)
+#endif
   switch (Mt.kind) {
     case 0:  // lightSource: emit, Absorb
       L = L + T * tex;
