@@ -290,7 +290,9 @@ def spawn_ranks(n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=30,
+                    help="timed frames (default 30: the Cornell frame is ~5 ms, so the barrier and "
+                         "synchronise around the timed region weigh < 0.5 %)")
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="cornell", choices=["cornell", "readme", "demo1", "demo1_1200x800", "bunny_cornell", "pawn_fog"])
     ap.add_argument("--row-block", type=int, default=1,
