@@ -1004,7 +1004,12 @@ void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_s
   // Cornell / pawn+fog at 1 GPU: -2.4 % / -1 %); with fewer than ~64 items per resident lane (an
   // 8-GPU rank's share, the Cornell box) the longer last items cost more than that (bunny at 8
   // shards: 20.7 -> 22.0 ms), so those keep 4.
-  int chunk = spp < 4 ? spp : 4;
+  // The flat kernel's small (tail) items hold 3 samples since round 4 (one-wave workgroups, 5 / 8
+  // waves per SIMD): Cornell 5.045 -> 4.992 ms binary64 at 1 GPU, one rank's share of 8 0.715 ->
+  // 0.706, README's share of 8 0.161 -> 0.134, README at 1 GPU 0.620 -> 0.628 (+1.3 %);
+  // profiles/r4/chunk_sweep.  The BVH kernels keep 4.
+  const int small = two_sizes ? 3 : 4;
+  int chunk = spp < small ? spp : small;
   if (resident_lanes > 0 && (long long)P.tile_rows * P.cam.width * spp / 16 >= 64 * resident_lanes) chunk = 16;
   if (const char* env = rt_knob("RT_AMD_CHUNK")) {  // tuning knob for experiments
     int c = std::atoi(env);
