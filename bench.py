@@ -393,6 +393,10 @@ def main():
         works = [None] * nbuf
         streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(args.streams - 1)]
         ev = []
+        # N > 1 over RCCL: per timed frame, the gather's completion seen from a probe stream that only
+        # waits for it (the compute streams never wait on the probe): render end -> gather done
+        probe = torch.cuda.Stream(dev) if n > 1 and args.dist_backend == "nccl" else None
+        gev = []
         frame = [0]
 
         def step(timed):
@@ -418,6 +422,12 @@ def main():
             if n > 1:
                 if args.dist_backend == "nccl":
                     works[b] = dist.all_gather_into_tensor(gathered[b], tile, async_op=True)
+                    if timed:
+                        with torch.cuda.stream(probe):
+                            works[b].wait()
+                            g = torch.cuda.Event(enable_timing=True)
+                            g.record(probe)
+                        gev.append((e1, g))
                 else:  # rehearsal path: through host memory
                     parts = [torch.empty((rows, w, 3), dtype=dtype) for _ in range(n)]
                     dist.all_gather(parts, tile.cpu())
@@ -462,7 +472,7 @@ def main():
         if n > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
-        elapsed = time.perf_counter() - t0
+        elapsed = elapsed_local = time.perf_counter() - t0
         if n > 1:
             t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -489,8 +499,23 @@ def main():
                      "mean_rgb": [round(float(x), 5) for x in img.reshape(-1, 3).mean(0)],
                      # digest of the assembled frame's bytes: equal across GPU counts (bit-identical)
                      "sha16": hashlib.sha256(np.ascontiguousarray(img).tobytes()).hexdigest()[:16]}
+        # per rank (N > 1): which rank and which phase set the max-over-ranks time — its render
+        # kernel time per frame, the gathers' completion after its renders, its own wall time
+        ranks = None
+        if n > 1:
+            mine = {"rank": rank, "kernel_ms": round(kernel_ms, 4), "launch_ms": round(launch_ms, 4),
+                    "gather_after_render_ms": round(sum(a.elapsed_time(b) for a, b in gev) / len(gev), 4) if gev else None,
+                    "ms_per_step_local": round(elapsed_local / args.steps * 1e3, 4)}
+            allr = [None] * n
+            dist.all_gather_object(allr, mine)
+            km = [r["kernel_ms"] for r in allr]
+            ranks = {"per_rank": allr, "kernel_ms_min": min(km), "kernel_ms_max": max(km),
+                     "slowest_rank": max(allr, key=lambda r: r["ms_per_step_local"])["rank"],
+                     "note": "kernel_ms: the rank's render device time per frame (HIP events); gather_after_render_ms: "
+                             "a frame's render end -> its RCCL all_gather done (probe stream, RCCL only); "
+                             "ms_per_step_local: the rank's own timed region / frames before the max over ranks"}
         return dict(elapsed=elapsed, launch_ms=launch_ms, kernel_ms=kernel_ms, warm_frames=warm_frames,
-                    warm_s=warm_s, check=check, streams=len(streams))
+                    warm_s=warm_s, check=check, streams=len(streams), ranks=ranks)
 
     precisions = [args.precision] + (["f32"] if args.precision == "f64" and not args.no_f32 else [])
     res = {p: measure(p) for p in precisions}
@@ -510,7 +535,7 @@ def main():
                            "warmup_frames": r["warm_frames"], "warmup_s": round(r["warm_s"], 3),
                            "roofline": roofline_of(args.config, p, r["kernel_ms"], r["launch_ms"], share,
                                                    samples_per_launch, r["streams"]),
-                           "check": r["check"]}
+                           "check": r["check"], "ranks": r["ranks"]}
         value, main_rec = record(precisions[0])
         cpu = None
         if n == 1 and not args.no_cpu_baseline:
@@ -534,6 +559,8 @@ def main():
                                       + (f" (diagnostic: shard 0 of {n_sh} only)" if n_sh != n else "")},
             "roofline": main_rec["roofline"], "cpu_baseline": cpu, "check": main_rec["check"],
         }
+        if main_rec["ranks"] is not None:
+            line["ranks"] = main_rec["ranks"]
         if len(precisions) > 1:
             _, f32 = record("f32")
             f32["note"] = "FP32 fast path (rt_exec.flags RT_EXEC_F32), same frames, measured after the f64 line"

@@ -499,6 +499,10 @@ int multi_render(rt_multi_scene* M, const rt_camera_settings* cs, uint64_t seed,
     int allocs = 0;
   };
   std::vector<Job> jobs(n);
+  // experiments and tests: shards forced onto the tile + strided-copy path a device without peer
+  // access takes (RT_AMD_COPY_SHARDS: bit k for shard k, -1 every shard), so one GPU exercises it
+  unsigned long long copy_mask = 0;
+  if (const char* e = rt_knob("RT_AMD_COPY_SHARDS")) copy_mask = (unsigned long long)strtoll(e, nullptr, 0);
   for (int k = 0; k < n; ++k) {
     Job& p = jobs[k];
     p.ex = *ex;
@@ -546,7 +550,7 @@ int multi_render(rt_multi_scene* M, const rt_camera_settings* cs, uint64_t seed,
           const size_t tile_pixels = (size_t)p.rows * cs->image_width;
           // n > 1: the resolve writes the shard's rows straight into the frame on the first device
           // (over xGMI from a peer); without peer access, a tile and a strided copy
-          const bool direct = n > 1 && M->peer_ok[M->scene_of[k]];
+          const bool direct = n > 1 && M->peer_ok[M->scene_of[k]] && !((copy_mask >> k) & 1ull);
           if (!direct)
             if (int r = grow(&q.d_tile, &q.tile_cap, tile_pixels * 3 * esize, &p.allocs)) return r;
           const size_t wsb = workspace_bytes(tile_pixels, f32 ? RT_ACC_WORDS(float) : RT_ACC_WORDS(double), nullptr, nullptr);
@@ -773,6 +777,14 @@ int rt_encode8_async(const void* d_rgb, int32_t in_f64, uint8_t* d_out, int64_t 
 // diagnostic build only: the BVH kernel's phase counters (rt_trace.h RT_PHASE_PROF), read and zeroed
 int rt_prof_read(int f64, unsigned long long* out, int n) {
   return f64 ? rt_prof_read_kernel((const KernelParams64*)nullptr, out, n) : rt_prof_read_kernel((const KernelParams*)nullptr, out, n);
+}
+#endif
+#if defined(RT_WAVE_STAMPS)
+// diagnostic build only: per-wave (start, queue drained, end, hw id) stamps of the last renders
+// (rt_render_kernel.h RT_WAVE_STAMPS), read and zeroed; returns the waves read
+int rt_stamps_read(int f64, unsigned long long* out, int n_waves) {
+  return f64 ? rt_stamps_read_kernel((const KernelParams64*)nullptr, out, n_waves)
+             : rt_stamps_read_kernel((const KernelParams*)nullptr, out, n_waves);
 }
 #endif
 

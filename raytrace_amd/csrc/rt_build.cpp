@@ -878,8 +878,9 @@ int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, boo
                    (mats ? RT_VAR_MATS : 0) | (tex ? RT_VAR_TEX : 0);  // two-level traversal: the decoupled BVH loop
   if (const char* e = rt_knob("RT_AMD_VARIANT")) {
     const int f = atoi(e);
-    if (!flat && (f == RT_VAR_BVH_LOCKSTEP || f == RT_VAR_BVH)) v = f;  // flat scenes run on any variant
-    if (flat && f >= RT_VAR_FLAT && f <= RT_VAR_BVH) v = f;
+    // (the lockstep kernels exist only in experiment builds, RT_LOCKSTEP_KERNELS)
+    const bool ok = f == RT_VAR_BVH || (RT_LOCKSTEP_KERNELS && f == RT_VAR_BVH_LOCKSTEP) || (flat && f == RT_VAR_FLAT);
+    if (ok) v = f;  // flat scenes run on any variant
   }
   // one-class BVH leaves: the decoupled kernel (leaf_kind covers the leaves below BVH nodes of the
   // surface and media sets; the kernel dispatch keeps the generic test where no one-class

@@ -99,6 +99,12 @@
 // render-kernel variants (rt_kernel.hip)
 #define RT_VAR_FLAT 0          // every set one flat leaf, lockstep lane loop
 #define RT_VAR_BVH_LOCKSTEP 1  // BVH, lockstep lane loop (reference schedule; experiments and tests)
+// The lockstep BVH kernels are compiled only into experiment builds (make exp DEFS=
+// -DRT_LOCKSTEP_KERNELS=1) and the host emulator: the product library's RT_AMD_VARIANT=1 runs the
+// decoupled kernel
+#ifndef RT_LOCKSTEP_KERNELS
+#define RT_LOCKSTEP_KERNELS 0
+#endif
 #define RT_VAR_BVH 2           // BVH, traversal decoupled from shading (default for BVH scenes)
 #define RT_VAR_BASE 3
 #define RT_VAR_NOISE 4         // flag: the scene has noise / marble textures (their code compiled in)
@@ -409,6 +415,10 @@ int rt_launch_resolve(const KernelParams64& p, void* stream);
 #if defined(RT_PHASE_PROF)
 int rt_prof_read_kernel(const KernelParams*, unsigned long long* out, int n);
 int rt_prof_read_kernel(const KernelParams64*, unsigned long long* out, int n);
+#endif
+#if defined(RT_WAVE_STAMPS)
+int rt_stamps_read_kernel(const KernelParams*, unsigned long long* out, int n_waves);
+int rt_stamps_read_kernel(const KernelParams64*, unsigned long long* out, int n_waves);
 #endif
 // 8-bit epilogue over float (in_f64 = 0) or binary64 (1) values; thr: 256 host thresholds
 int rt_launch_encode8(const void* in, int in_f64, uint8_t* out, int64_t n, const double* thr, int encoding,

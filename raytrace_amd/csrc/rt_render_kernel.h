@@ -21,6 +21,16 @@
 #define RT_ACC_LDS_OF(kVar, kMedia) (RT_ACC_IN_LDS && (kVar) != RT_VAR_FLAT && (RT_F64 || !(kMedia)))
 
 namespace RT_NS {
+
+// Diagnostic build only (make exp DEFS=-DRT_WAVE_STAMPS, tools/wave_stamps.py): per wave the
+// wall clock (s_memrealtime, 100 MHz) at its start, when its grab first finds every queue spent
+// (the queue has drained: from then on the wave only finishes the items it holds) and at its end,
+// and its hardware id — the ramp and the tail of one launch, wave by wave.
+#if defined(RT_WAVE_STAMPS)
+#define RT_STAMP_WAVES 16384
+__device__ unsigned long long rt_stamp_buf[4 * RT_STAMP_WAVES];
+#endif
+
 namespace {
 
 // Item claims.  A wave keeps a pool of consecutive item ids in SGPRs (wave-uniform state) and
@@ -38,6 +48,16 @@ static_assert(RT_POOL >= 64, "a refill must cover every lane of a wave");
 // 3.455 / 3.42 / 3.42 / 3.43, Cornell's 8-GPU share 0.520 / 0.517 / 0.517 / 0.519.
 #ifndef RT_QUEUES
 #define RT_QUEUES 4
+#endif
+// How the queues split the dynamic ids.  Contiguous quarters (0, rounds 3-4) put the big items
+// (the first ids) in the first queues and the small tail items in the last: the waves of a spent
+// queue move on to the next, so the frame ENDED on the big items of the last queue to drain — the
+// per-wave stamps of one binary64 Cornell launch (tools/wave_stamps.py, profiles/r5/) showed the
+// queue drained at 4.78 ms and the last wave ending 1.30 ms later.  Interleaved pools (1): queue q
+// serves pools q, q + RT_QUEUES, ... of RT_POOL ids, so every queue walks the ids in order and the
+// tail items come last, as rt_host_plan_work intends.
+#ifndef RT_QUEUE_INTERLEAVE
+#define RT_QUEUE_INTERLEAVE 1
 #endif
 static_assert((RT_QUEUES & (RT_QUEUES - 1)) == 0 && RT_QUEUES <= 8, "RT_QUEUES: a power of two, at most 8 (workspace)");
 // Per-wave commit aggregation.  Ids are pixel-major (rt_trace.h open_item), so the RT_POOL
@@ -88,6 +108,9 @@ struct WaveWork {
   unsigned long long* slots;
   int* hdr;
   unsigned free_mask;  // wave-uniform
+#if defined(RT_WAVE_STAMPS)
+  unsigned long long t_drain = 0;  // wall clock when every queue was first found spent
+#endif
   // the kernel arguments re-read where used (rt_trace.h RT_KARGS): not held across the lane loop
   __device__ __forceinline__ const KernelParams& kp() const { return RT_KARGS_IF(kReread, P); }
 
@@ -151,18 +174,39 @@ struct WaveWork {
     pool_left = 0;
     const int leader = __ffsll((unsigned long long)m) - 1;
     const int dyn = n_items - offset;
+#if RT_QUEUE_INTERLEAVE
+    const int n_pools = dyn > 0 ? (dyn + RT_POOL - 1) / RT_POOL : 0;
+#else
     const int len = dyn > 0 ? (dyn + RT_QUEUES - 1) / RT_QUEUES : 0;
+#endif
     while (rest > 0 && spent < RT_QUEUES) {
+#if RT_QUEUE_INTERLEAVE
+      // queue q hands out the dynamic pools q, q + RT_QUEUES, q + 2 RT_QUEUES, ... (one counter
+      // increment per pool): the ids are claimed in (nearly) global order whatever queue a wave
+      // draws from, so the frame ends with the last, smallest items
+      int pk = 0;
+      if (lane == leader) pk = atomicAdd(kp().counter + 64 * queue, 1);
+      pk = __builtin_amdgcn_readfirstlane(__shfl(pk, leader));
+      const int qs = offset, qlen = dyn;
+      if (pk * RT_QUEUES + queue >= n_pools) {  // spent: the queue's next pool is past the last one
+#else
       const int qs = offset + queue * len;
       const int qlen = min(len, n_items - qs);  // <= 0 for an empty last queue
       int base = 0;
       if (lane == leader) base = atomicAdd(kp().counter + 64 * queue, RT_POOL);
       base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
       if (base >= qlen) {  // spent: ids are only ever handed out below qlen
+#endif
         queue = (queue + 1) & (RT_QUEUES - 1);
         ++spent;
+#if defined(RT_WAVE_STAMPS)
+        if (spent == RT_QUEUES && t_drain == 0) t_drain = wall_clock64();
+#endif
         continue;
       }
+#if RT_QUEUE_INTERLEAVE
+      const int base = (pk * RT_QUEUES + queue) * RT_POOL;
+#endif
       const int avail = min(RT_POOL, qlen - base);
       const int take = min(rest, avail);
       pool_slot = open_pool(qs + base, avail);
@@ -174,7 +218,7 @@ struct WaveWork {
       rest -= take;
       pool_base = qs + base + take;
       pool_left = avail - take;
-      if (rest > 0) {  // the pool ended at the queue's end
+      if (rest > 0) {  // the pool ended at the queue's end (interleaved: the last, short pool)
         queue = (queue + 1) & (RT_QUEUES - 1);
         ++spent;
       }
@@ -331,6 +375,9 @@ __global__ __launch_bounds__(RT_BLOCK_OF(kVar, kTex, kMedia, kMats))
 __attribute__((amdgpu_waves_per_eu(RT_WAVES_OF(kVar, kTex, kMedia, kMats))))
 void rt_render_kernel(KernelParams P) {
   extern __shared__ int smem[];
+#if defined(RT_WAVE_STAMPS)
+  const unsigned long long t_start = wall_clock64();
+#endif
   constexpr int kSlots = RT_AGG_SLOTS_OF(kVar), kPix = RT_AGG_PIX_OF(kVar);
   constexpr int kBlock = RT_BLOCK_OF(kVar, kTex, kMedia, kMats);
   constexpr int kAggBytes = AggGeom<kSlots, kPix>::kWaveBytes;
@@ -354,10 +401,24 @@ void rt_render_kernel(KernelParams P) {
   unsigned long long* agg = reinterpret_cast<unsigned long long*>(smem_rest) + kAggBytes / 8 * wave_in_block;
   smem_rest += kAggBytes / 4 * (int)(blockDim.x / 64);
   for (int i = (int)__lane_id(); i < kAggBytes / 8; i += 64) agg[i] = 0ull;
+#if defined(RT_WAVE_STAMPS)
+  // (vector stores from lane 0; waves beyond the buffer are not recorded)
+#define RT_STAMP_END(work)                                                                        \
+  if (__lane_id() == 0 && wave < RT_STAMP_WAVES) {                                                \
+    rt_stamp_buf[4 * wave] = t_start;                                                             \
+    rt_stamp_buf[4 * wave + 1] = work.t_drain;                                                    \
+    rt_stamp_buf[4 * wave + 2] = wall_clock64();                                                  \
+    rt_stamp_buf[4 * wave + 3] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (31 << 11)) << 32 | \
+                                 (unsigned)__builtin_amdgcn_s_getreg((20 << 0) | (3 << 11));      \
+  }
+#else
+#define RT_STAMP_END(work)
+#endif
   if constexpr (kVar == RT_VAR_FLAT) {
     WaveWork<kSlots, kPix, true> work(P, wave, waves, agg);
     overflow = lane_loop_lockstep<true, kTex, kMedia, kMats>(P, work, Trav{nullptr, 0, nullptr}, P.prims, acc);
     work.finish();
+    RT_STAMP_END(work)
   } else {
     v4f* lds_nodes = reinterpret_cast<v4f*>(smem_rest + (P.stack_depth + 1) * kBlock);
     const float4* src = reinterpret_cast<const float4*>(P.nodes);
@@ -373,6 +434,7 @@ void rt_render_kernel(KernelParams P) {
     else
       overflow = lane_loop_bvh<kTex, kMedia, kMats, kInst, kLeaf>(P, work, W, P.prims, acc);
     work.finish();
+    RT_STAMP_END(work)
   }
   if (overflow) atomicOr(P.status, 1);
 }
@@ -479,7 +541,9 @@ static render_fn render_kernel_of(int variant) {
   if (variant & RT_VAR_INST) return render_kernel_flags<RT_VAR_BVH, true>(variant);
   switch (variant & RT_VAR_BASE) {
     case RT_VAR_FLAT: return render_kernel_flags<RT_VAR_FLAT, false>(variant);
+#if RT_LOCKSTEP_KERNELS
     case RT_VAR_BVH_LOCKSTEP: return render_kernel_flags<RT_VAR_BVH_LOCKSTEP, false>(variant);
+#endif
     default: return render_kernel_flags<RT_VAR_BVH, false>(variant);
   }
 }
@@ -536,6 +600,20 @@ int rt_prof_read_kernel(const KernelParamsT<RT_NS::real>*, unsigned long long* o
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rt_prof_buf), n * sizeof(unsigned long long)) != hipSuccess) return -1;
   unsigned long long zero[PF_N] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(rt_prof_buf), zero, sizeof(zero)) == hipSuccess ? n : -1;
+}
+#endif
+
+#if defined(RT_WAVE_STAMPS)
+// diagnostic build: read (and zero) this precision's per-wave stamps, 4 words per wave
+int rt_stamps_read_kernel(const KernelParamsT<RT_NS::real>*, unsigned long long* out, int n_waves) {
+  using namespace RT_NS;
+  if (n_waves > RT_STAMP_WAVES) n_waves = RT_STAMP_WAVES;
+  const size_t bytes = 4 * sizeof(unsigned long long) * (size_t)n_waves;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rt_stamp_buf), bytes) != hipSuccess) return -1;
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(rt_stamp_buf)) != hipSuccess) return -1;
+  return hipMemset(p, 0, sizeof(rt_stamp_buf)) == hipSuccess ? n_waves : -1;
 }
 #endif
 

@@ -1008,7 +1008,8 @@ RT_FN Acc acc_words(const AccLds& A) {
 // rt_prof_buf.
 #if defined(RT_PHASE_PROF) && !defined(RT_HOST_EMU)
 enum : int { PF_FRONT, PF_TRAV, PF_SHADE, PF_ITERS, PF_ROUNDS, PF_TRACING, PF_LIVE, PF_SHADING, PF_FRONT_LANES,
-             PF_NODE_STEPS, PF_NODE_LANES, PF_LEAF_STEPS, PF_LEAF_LANES, PF_NODE_CLK, PF_LEAF_CLK, PF_N };
+             PF_NODE_STEPS, PF_NODE_LANES, PF_LEAF_STEPS, PF_LEAF_LANES, PF_NODE_CLK, PF_LEAF_CLK, PF_CAM,
+             PF_CAM_LANES, PF_N };
 __device__ unsigned long long rt_prof_buf[PF_N];
 #define RT_PROF_DECL unsigned long long prof[PF_N] = {}; unsigned long long pf_t0 = clock64(), pf_t1;
 #define RT_PROF_MARK(k) (pf_t1 = clock64(), prof[k] += pf_t1 - pf_t0, pf_t0 = pf_t1)
@@ -1442,7 +1443,7 @@ RT_FN bool shade_event(const KernelParams& P, cfp prims, uint32_t pix, int sampl
   if (need_tex) tex = eval_texture<kTex == 2>(P, Mt.tex, h.u, h.v, h.p);
   u4 w = philox(pix, (uint32_t)sample, (uint32_t)seg, RT_EV_SCATTER, P.key0, P.key1);
 #ifdef RT_HOST_EMU
-  f3 newdir = R.d;  // (defined on every path on the CPU)
+  f3 newdir = mk3(RT_NAN, RT_NAN, RT_NAN);  // poison on the CPU: read only where the path goes on
 #else
   f3 newdir;  // set where the path goes on (the caller reads it only there)
 #endif
@@ -1562,14 +1563,20 @@ RT_FN bool shade_event(const KernelParams& P, cfp prims, uint32_t pix, int sampl
 // throughput factor and self id are defined only where the path goes on (no exit of shade_event
 // carries the unchanged ray to a join), and the loop-carried ray and throughput are written
 // unconditionally: a path that ends is restarted by camera_ray (origin, direction, self ids) with
-// a fresh throughput and segment count before anything reads them.  In the flat binary64 kernel
+// a fresh throughput and segment count before anything reads them.  INVARIANT of the lane loops
+// (lane_loop_lockstep, lane_loop_bvh): after shade returns true, R, T and the self ids are
+// indeterminate (the GPU builds leave them unset, the host emulator poisons them with NaN) and
+// nothing may read them before camera_ray.  In the flat binary64 kernel
 // the joins' copies were ~40 v_mov per lane-loop iteration, and selects in their place ~20.
 template <int kTex, bool kMats, bool kInst = false>
 RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int& seg, real tbest, int best,
                  int hit_medium, RayCtx& R, f3& L, f3& T, int best_inst = -1) {
 #ifdef RT_HOST_EMU
-  f3 np = R.o, nd = R.d, Tf = mk3(RL(1.), RL(1.), RL(1.));  // (defined on the CPU too)
-  int ngid = R.self_gid;
+  // poison on the CPU: a path that ends leaves R, T and the self ids undefined (NaN / an id no leaf
+  // has) until camera_ray restarts it, so an emulator test fails if anything reads them in between
+  const real nan = RT_NAN;
+  f3 np = mk3(nan, nan, nan), nd = np, Tf = np;
+  int ngid = RT_EMPTY_ROOT;
 #else
   f3 np, nd, Tf;
   int ngid;
@@ -1650,9 +1657,12 @@ RT_FN int lane_loop_lockstep(const KernelParams& P0, Work& work, const Trav& TW,
   R.time = RL(0.0);
   R.self_gid = -1;
   R.self_inst = -1;
+  RT_PROF_DECL
   for (;;) {
     const KernelParams& P = RT_KARGS(P0);  // (per iteration: RT_KARGS)
     const bool need = !alive && I.sample >= I.s_end;
+    RT_PROF_ADD(PF_ITERS, 1);
+    RT_PROF_ADD(PF_FRONT_LANES, RT_BALLOT_COUNT(need));
     work.commit(need && I.tp != -1, I.tp, acc, bad);
     int aslot;
     const int got = work.grab(need, aslot);
@@ -1664,6 +1674,8 @@ RT_FN int lane_loop_lockstep(const KernelParams& P0, Work& work, const Trav& TW,
       I.tp = work.tag(I.tp, aslot);
       if (!ok) continue;
     }
+    RT_PROF_MARK(PF_FRONT);
+    RT_PROF_ADD(PF_CAM_LANES, RT_BALLOT_COUNT(!alive));
     if (!alive) {
       camera_ray(P, I.pix, I.sample, I.pxgy, R);
       L = mk3(RL(0.), RL(0.), RL(0.));
@@ -1671,6 +1683,7 @@ RT_FN int lane_loop_lockstep(const KernelParams& P0, Work& work, const Trav& TW,
       seg = 0;
       alive = true;
     }
+    RT_PROF_MARK(PF_CAM);
     RT_COUNT(2);
     // ---- closest hit over the surfaces and every medium (Ray.hs:178)
     if constexpr (!kFlat) prep_ray(R);  // reciprocal direction: BVH slab tests only
@@ -1707,13 +1720,17 @@ RT_FN int lane_loop_lockstep(const KernelParams& P0, Work& work, const Trav& TW,
       }
       medium_event(P, m, I.pix, I.sample, seg, lo, hi, tbest, hit_medium);
     }
+    RT_PROF_MARK(PF_TRAV);
     if (shade<kTex, kMats>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T)) {
+      // the path ended: R and T are indeterminate until camera_ray (shade's invariant)
       RT_HOOK_SAMPLE(I.pix, I.sample, L);
       acc_sample(acc, L, bad);
       alive = false;
       ++I.sample;
     }
+    RT_PROF_MARK(PF_SHADE);
   }
+  RT_PROF_FLUSH
   return overflow;
 }
 
@@ -1865,6 +1882,7 @@ RT_FN int lane_loop_bvh(const KernelParams& P0, Work& work, const Trav& TW, cons
       const KernelParams& P = RT_KARGS(P0);
       f3 L = mk3(RL(0.), RL(0.), RL(0.));
       if (shade<kTex, kMats, kInst>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T, best_inst)) {
+        // the path ended: R and T are indeterminate until camera_ray (shade's invariant)
         RT_HOOK_SAMPLE(I.pix, I.sample, L);
         acc_sample(acc, L, bad);
         ++I.sample;

@@ -5,9 +5,12 @@ import sys
 import numpy as np
 import pytest
 
-# the tests that compare code paths set the library's RT_AMD_* knobs, which it reads only with the
-# experiments switch on (rt_internal.h rt_knob; test_host_mirror checks it is ignored without)
-os.environ.setdefault("RT_AMD_EXPERIMENTS", "1")
+# The tests run the library as callers get it: stray RT_AMD_* variables of the environment (an A/B
+# session's knobs, RT_AMD_LIB, the experiments switch) are dropped at session start.  The tests that
+# compare code paths set knobs through the `knobs` fixture, which turns the switch on for that test
+# only (rt_internal.h rt_knob; test_host_mirror checks the knobs are ignored without it).
+for _k in [k for k in os.environ if k.startswith("RT_AMD_")]:
+    del os.environ[_k]
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
@@ -19,6 +22,13 @@ for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests", "kerne
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
     config.addinivalue_line("markers", "slow: long CPU test")
+
+
+@pytest.fixture
+def knobs(monkeypatch):
+    """The library's RT_AMD_* experiment knobs honoured for this test (set them with monkeypatch)."""
+    monkeypatch.setenv("RT_AMD_EXPERIMENTS", "1")
+    return monkeypatch
 
 
 @pytest.fixture(scope="session")

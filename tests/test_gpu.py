@@ -252,9 +252,11 @@ def test_full_demo1_is_finite(gpu, precision):
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("name", ["cornell", "pawn_fog", "bunny_cornell", "demo1"])
-def test_kernel_variants_bitwise_identical(gpu, monkeypatch, name, precision):
-    """Flat / BVH-lockstep / BVH-decoupled kernels: same per-path arithmetic, different schedule;
-    fixed-point accumulation makes the images bit-identical."""
+def test_kernel_variants_bitwise_identical(knobs, gpu, monkeypatch, name, precision):
+    """Flat / BVH-decoupled kernels: same per-path arithmetic, different schedule; fixed-point
+    accumulation makes the images bit-identical.  (The lockstep BVH kernel, the reference schedule,
+    is compiled into experiment builds only, RT_LOCKSTEP_KERNELS; the host emulator checks it,
+    test_oracle_golden.py test_kernel_variants_render_bitwise_identical_images.)"""
     fn = {"cornell": scenes.cornell_box, "pawn_fog": scenes.pawn_fog, "bunny_cornell": scenes.bunny_cornell,
           "demo1": scenes.demo1}[name]
     cs, world, seed = fn(width=96, spp=8)
@@ -262,7 +264,7 @@ def test_kernel_variants_bitwise_identical(gpu, monkeypatch, name, precision):
     # the flat kernel tests cuboid faces as box groups, the BVH kernels run on a flat scene test
     # them one by one (same result up to rounding at the box edges): compare with box groups off
     monkeypatch.setenv("RT_AMD_NO_BOX", "1")
-    for v in ("0", "1", "2"):
+    for v in ("0", "2"):
         monkeypatch.setenv("RT_AMD_VARIANT", v)
         imgs.append(R.raytrace(cs, world, seed, precision=precision))
     for img in imgs[1:]:
@@ -271,7 +273,7 @@ def test_kernel_variants_bitwise_identical(gpu, monkeypatch, name, precision):
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("name", ["bunny_cornell", "demo1"])
-def test_large_primitive_prefix_is_exact(gpu, monkeypatch, name, precision):
+def test_large_primitive_prefix_is_exact(knobs, gpu, monkeypatch, name, precision):
     fn = {"bunny_cornell": scenes.bunny_cornell, "demo1": scenes.demo1}[name]
     cs, world, seed = fn(width=96, spp=8)
     monkeypatch.setenv("RT_AMD_NO_BOX", "1")  # exact claim: per-face tests in and out of the BVH
@@ -283,7 +285,7 @@ def test_large_primitive_prefix_is_exact(gpu, monkeypatch, name, precision):
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("name", ["cornell", "box_gallery"])
-def test_box_groups_match_oracle(gpu, oracle_mod, monkeypatch, name, precision):
+def test_box_groups_match_oracle(knobs, gpu, oracle_mod, monkeypatch, name, precision):
     fn = {"cornell": scenes.cornell_box, "box_gallery": scenes.box_gallery}[name]
     cs, world, seed = fn(width=96, spp=8)
     a = R.raytrace(cs, world, seed, precision=precision)
@@ -300,7 +302,7 @@ def test_box_groups_match_oracle(gpu, oracle_mod, monkeypatch, name, precision):
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("name", ["cornell", "bunny_cornell"])
-def test_item_chunk_does_not_change_the_image(gpu, monkeypatch, name, precision):
+def test_item_chunk_does_not_change_the_image(knobs, gpu, monkeypatch, name, precision):
     """Items of 1, 3 (ragged: does not divide spp), 4 and 16 samples, and two item sizes: a
     different work split and commit order, the same fixed-point sums — bit-identical images."""
     fn = {"cornell": scenes.cornell_box, "bunny_cornell": scenes.bunny_cornell}[name]
@@ -320,7 +322,7 @@ def test_item_chunk_does_not_change_the_image(gpu, monkeypatch, name, precision)
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("name", ["cornell", "bunny_cornell", "pawn_fog"])
-def test_commit_aggregation_is_exact(gpu, monkeypatch, name, precision):
+def test_commit_aggregation_is_exact(knobs, gpu, monkeypatch, name, precision):
     """Items summed per pixel in the waves' LDS slots before the commit atomics (rt_render_kernel.h
     WaveWork) against every item committed directly (RT_AMD_AGG=0): bit-identical images, with one
     item size (32 / 128 chunks per pixel: flat and BVH kernels aggregate) and with two sizes (a
@@ -342,7 +344,7 @@ def test_commit_aggregation_is_exact(gpu, monkeypatch, name, precision):
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("name", ["bunny_cornell", "demo1", "pawn_fog"])
-def test_one_class_leaf_kernels_are_exact(gpu, monkeypatch, name, precision):
+def test_one_class_leaf_kernels_are_exact(knobs, gpu, monkeypatch, name, precision):
     """BVH kernels whose leaf test is specialised to the scene's one primitive class (RT_VAR_LEAF_TRI
     for the bunny and for pawn+fog — its media kernel, the fog sphere a single-leaf medium set
     tested generically — RT_VAR_LEAF_SPHERE for demo1) against the generic leaf test: the same
@@ -356,7 +358,7 @@ def test_one_class_leaf_kernels_are_exact(gpu, monkeypatch, name, precision):
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
-def test_medium_boundary_alias_is_exact(gpu, monkeypatch, precision):
+def test_medium_boundary_alias_is_exact(knobs, gpu, monkeypatch, precision):
     cs, world, seed = scenes.pawn_fog(width=96, spp=8)
     a = R.raytrace(cs, world, seed, precision=precision)
     monkeypatch.setenv("RT_AMD_NO_ALIAS", "1")
@@ -468,6 +470,55 @@ def test_multi_device_scene_allocates_once(gpu, precision):
     assert st[2]["device_allocs"] == 1, st  # the 8-bit buffer, once
     assert st[3]["device_allocs"] > 0 and again["device_allocs"] == 0, (st, again)
     m.close()
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_multi_device_copy_path(knobs, gpu, monkeypatch, precision):
+    """The path of a shard whose device has no peer access to the first one (rt_api.hip
+    multi_render: its own tile, then one strided hipMemcpy2DAsync into the frame), forced on one GPU
+    with RT_AMD_COPY_SHARDS (bit k: shard k): every shard copied, and copied and direct shards
+    writing the same frame.  Bit-identical to the one-device render, linear and encoded; the first
+    render allocates the workspaces, the copied shards' tiles and the frame, the next ones nothing."""
+    cs, world, seed = scenes.bunny_cornell(width=48, spp=2)
+    a = R.raytrace(cs, world, seed, precision=precision)
+    for devs, mask in (([0, 0], "-1"), ([0, 0, 0], "-1"), ([0, 0, 0], "0x5"), ([0] * 4, "0x2")):
+        monkeypatch.setenv("RT_AMD_COPY_SHARDS", mask)
+        m = R.MultiDeviceScene(world, devs)
+        try:
+            st = [{}, {}]
+            for k in range(2):
+                np.testing.assert_array_equal(m.render(cs, seed, precision=precision, row_block=2, stats=st[k]), a)
+            np.testing.assert_array_equal(m.render(cs, seed, precision=precision, row_block=1), a)
+            np.testing.assert_array_equal(m.render(cs, seed, precision=precision, encode="sqrt"), R.encode8(a, "sqrt"))
+        finally:
+            m.close()
+        copied = len(devs) if mask == "-1" else bin(int(mask, 0)).count("1")
+        assert st[0]["device_allocs"] == len(devs) + copied + 1, (devs, mask, st)
+        assert st[1]["device_allocs"] == 0, (devs, mask, st)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_multi_device_distinct_gpus(gpu, precision):
+    """A device list over DISTINCT GPUs: each peer device's resolve writes its rows straight into the
+    first device's frame over xGMI (rt_api.hip multi_render).  [0, 1] and [0, 1, 0, 1], linear in
+    both precisions and 8-bit, rendered twice (the resident buffers re-used across devices), each
+    bit-identical to the one-device render.  Needs two GPUs: skipped on the one-GPU box, runs on the
+    driver's multi-GPU node."""
+    if gpu.cuda.device_count() < 2:
+        pytest.skip("needs two visible GPUs")
+    cs, world, seed = scenes.bunny_cornell(width=48, spp=2)
+    a = R.raytrace(cs, world, seed, precision=precision)
+    for devs in ([0, 1], [0, 1, 0, 1]):
+        m = R.MultiDeviceScene(world, devs)
+        try:
+            for rb in (1, 2):
+                st = {}
+                np.testing.assert_array_equal(m.render(cs, seed, precision=precision, row_block=rb, stats=st), a)
+            np.testing.assert_array_equal(m.render(cs, seed, precision=precision, encode="sqrt"), R.encode8(a, "sqrt"))
+            np.testing.assert_array_equal(m.render(cs, seed, precision=precision, encode="sqrt"), R.encode8(a, "sqrt"))
+        finally:
+            m.close()
+        assert st["device_allocs"] == 0, (devs, st)
 
 
 @pytest.mark.parametrize("name,precision", [("cornell", "f64"), ("cornell", "f32"), ("bunny_cornell", "f64")])

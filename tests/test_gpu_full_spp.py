@@ -4,8 +4,8 @@ test_gpu.py checks every config at full resolution but reduced spp (2-16).  The 
 the one that erodes with spp: every extra sample is another chance for a path to split on a
 decision within rounding of its threshold (a glass surface hit at a grazing angle, a total-
 internal-reflection test, a t-tie between two primitives).  Here each config renders at its
-BASELINE.json resolution AND spp (README 600x338x50, Cornell 600x600x200, demo1 1200x675x500,
-bunny-Cornell 800x800x1000, pawn+fog 800x800x2000) and is compared with the FP64 oracle
+BASELINE.json resolution AND spp (README 600x338x50, Cornell 600x600x200, demo1 1200x675x500 and
+1200x800x500, bunny-Cornell 800x800x1000, pawn+fog 800x800x2000) and is compared with the FP64 oracle
 (Philox mode: the same random numbers) on a sparse set of rows, sized so the oracle runs in
 seconds on the GPU box's 16 host cores.
 
@@ -35,7 +35,7 @@ from raytrace_amd import scenes  # noqa: E402
 from raytrace_amd.camera import image_height  # noqa: E402
 
 # (config, scene fn, row stride, L, per-sample split bound binary64, FP32).  Round 4: denser rows
-# (demo1 34, bunny-Cornell 40, pawn+fog 32) and bounds at ~3x the split rates measured on MI355X in
+# (demo1 34, bunny-Cornell 40, pawn+fog 32; round 5: pawn+fog 50, demo1 at 1200x800 40) and bounds at ~3x the split rates measured on MI355X in
 # round 3 (profiles/r3/parity_full_spp.jsonl, implied rate 1 - exact^(1/spp)): binary64 README 0,
 # Cornell 4.4e-7, demo1 1.34e-5 (glass spheres), bunny 3.1e-7, pawn+fog 0; FP32 3.1e-5, 1.7e-5,
 # 8.5e-6, 2.5e-6, 0.  Where none was measured the bound admits no more than a pixel or a few
@@ -44,8 +44,11 @@ CONFIGS = [
     ("readme", scenes.readme_scene, 4, 1.0, 3e-7, 1e-4),
     ("cornell", scenes.cornell_box, 8, 15.0, 1.3e-6, 5e-5),
     ("demo1", scenes.demo1, 20, 1.0, 4e-5, 2.5e-5),
+    # BASELINE.json config 3 at its stated size (1200x800, 500 spp; the reference renders demo1 at
+    # 1200x675, test/Main.hs:170-172): the same scene and bounds, 40 rows
+    ("demo1_1200x800", scenes.demo1_1200x800, 20, 1.0, 4e-5, 2.5e-5),
     ("bunny_cornell", scenes.bunny_cornell, 20, 15.0, 1e-6, 7.5e-6),
-    ("pawn_fog", scenes.pawn_fog, 25, 1.0, 1e-7, 1e-6),
+    ("pawn_fog", scenes.pawn_fog, 16, 1.0, 1e-7, 1e-6),  # 50 rows (round 4: 32)
 ]
 
 _REF = {}

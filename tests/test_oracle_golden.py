@@ -130,7 +130,7 @@ def test_glass_sphere_internal_reflection_chain_stays_finite(oracle_mod, emu_mod
 
 
 @pytest.mark.parametrize("name", ["cornell", "pawn_fog", "bunny_cornell"])
-def test_kernel_variants_render_bitwise_identical_images(emu_mod, monkeypatch, name):
+def test_kernel_variants_render_bitwise_identical_images(knobs, emu_mod, monkeypatch, name):
     """The three render-kernel variants (flat lockstep, BVH lockstep, BVH with traversal
     decoupled from shading) run the same per-path arithmetic in a different schedule; with
     fixed-point accumulation the images are bit-identical (host build of rt_trace.h)."""
@@ -148,7 +148,7 @@ def test_kernel_variants_render_bitwise_identical_images(emu_mod, monkeypatch, n
 
 
 @pytest.mark.parametrize("name", ["cornell", "readme"])
-def test_two_size_items_render_the_same_image(emu_mod, monkeypatch, name):
+def test_two_size_items_render_the_same_image(knobs, emu_mod, monkeypatch, name):
     """Work items of two sizes (flat kernel; rt_build.cpp rt_host_plan_work: big items for the
     first samples of every pixel, small ones for the tail; rt_trace.h open_item) cover every
     (pixel, sample) exactly once: with fixed-point sums the image is bit-identical to one item
@@ -163,7 +163,7 @@ def test_two_size_items_render_the_same_image(emu_mod, monkeypatch, name):
 
 
 @pytest.mark.parametrize("variant", ["1", "2"])
-def test_medium_boundary_alias_is_exact(emu_mod, monkeypatch, variant):
+def test_medium_boundary_alias_is_exact(knobs, emu_mod, monkeypatch, variant):
     """pawnTest's medium boundary is the dielectric surface itself; reusing the surface hit
     instead of traversing the boundary (DevMedium.alias_surface) gives the identical image."""
     cs, world, seed = scenes.pawn_fog(width=48, spp=4)
@@ -176,7 +176,7 @@ def test_medium_boundary_alias_is_exact(emu_mod, monkeypatch, variant):
 
 @pytest.mark.parametrize("variant", ["1", "2"])
 @pytest.mark.parametrize("name", ["bunny_cornell", "demo1"])
-def test_large_primitive_prefix_is_exact(emu_mod, monkeypatch, variant, name):
+def test_large_primitive_prefix_is_exact(knobs, emu_mod, monkeypatch, variant, name):
     """The surface set's large primitives (Cornell walls, demo1's ground sphere) tested before the
     BVH instead of inside it: the closest-hit key carries the global depth-first order, so the
     image is bit-identical, and the traversal does less work."""
@@ -193,7 +193,7 @@ def test_large_primitive_prefix_is_exact(emu_mod, monkeypatch, variant, name):
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("name,kind", [("bunny_cornell", 1), ("demo1", 2), ("pawn_fog", 1), ("pawn_test", 1), ("bunny_instances", 0)])
-def test_one_class_leaves_are_exact(emu_mod, monkeypatch, name, kind, precision):
+def test_one_class_leaves_are_exact(knobs, emu_mod, monkeypatch, name, kind, precision):
     """The host picks one-class leaf kernels from the leaves below BVH nodes (pawn+fog: the pawn's
     triangles in the surface and medium sets; its fog sphere is a single-leaf medium set, tested
     generically), and they render the generic kernel's image bit for bit."""
@@ -207,7 +207,7 @@ def test_one_class_leaves_are_exact(emu_mod, monkeypatch, name, kind, precision)
 
 
 @pytest.mark.parametrize("name", ["cornell", "box_gallery", "bunny_cornell"])
-def test_box_groups_match_per_face_tests(oracle_mod, emu_mod, monkeypatch, name):
+def test_box_groups_match_per_face_tests(knobs, oracle_mod, emu_mod, monkeypatch, name):
     """Cuboid faces and the Cornell walls tested as box groups (one slab test per box, DevBox)
     render the image of one parallelogram test per face up to FP32 rounding at the box edges,
     and match the FP64 oracle (which walks the reference's group of parallelograms) per pixel.

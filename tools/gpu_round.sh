@@ -15,7 +15,7 @@
 #              profiles/pmc_valu.json
 #   ab         tools/ab_libs.sh over AB_CFGS ("<config>:<sim-shards> ...") in PRECS, REPS repetitions
 #   image      tools/image_ab.py: images of each exp lib against the in-tree build, bit for bit
-#   phase      phase profile (needs raytrace_amd/_lib/exp/librt_amd_prof.so, -DRT_PHASE_PROF)
+#   phase      phase profile (needs raytrace_amd/_lib/diag/librt_amd_prof.so, -DRT_PHASE_PROF)
 #   microbench VALU rate / binary64 math microbenchmarks, built from source here
 #   rehearse   bench.py --gpus 2 / 3 on one GPU, frames bit-identical to N = 1
 #   shards     tools/shard_share_sweep.sh: one rank's share of an N-GPU frame, N = 1, 2, 4, 8
@@ -96,9 +96,14 @@ PY
         timeout -k 10 400 python3 tools/image_ab.py $lib $OUT/image_ab_$nm.json > $OUT/image_ab_$nm.log 2>&1 || { echo "image_ab $nm failed"; tail -20 $OUT/image_ab_$nm.log; exit 1; }
         echo "$nm: $(grep -c "'bit_identical': True" $OUT/image_ab_$nm.log) bit-identical of $(grep -c bit_identical $OUT/image_ab_$nm.log)"
       done ;;
+    stamps)  # needs raytrace_amd/_lib/diag/librt_amd_stamps.so (-DRT_WAVE_STAMPS)
+      for c in ${STAMP_CPS:-cornell:f64 cornell:f32}; do
+        RT_AMD_LIB=$PWD/raytrace_amd/_lib/diag/librt_amd_stamps.so timeout -k 10 200 python3 tools/wave_stamps.py ${c%%:*} ${c#*:} 5 >> $OUT/stamps.jsonl 2>> $OUT/stamps.err || { echo "stamps $c failed"; tail -5 $OUT/stamps.err; exit 1; }
+      done
+      python3 -c "import json,sys; [print(d['config'], d['precision'], d['median'], d['per_frame'][0]['ramp_ms'], d['per_frame'][0]['end_ms'], d['per_frame'][0]['alive_by_tenth']) for d in map(json.loads, open(sys.argv[1]))]" $OUT/stamps.jsonl ;;
     phase)
-      for c in "bunny_cornell f32" "bunny_cornell f64" "pawn_fog f64" "pawn_fog f32"; do
-        RT_AMD_LIB=$PWD/raytrace_amd/_lib/exp/librt_amd_prof.so timeout -k 10 300 python3 tools/phase_prof.py $c 2 >> $OUT/phase.jsonl 2>> $OUT/phase.err || { echo "phase $c failed"; tail -5 $OUT/phase.err; exit 1; }
+      for c in ${PHASE_CPS:-bunny_cornell:f32 bunny_cornell:f64 pawn_fog:f64 pawn_fog:f32}; do
+        RT_AMD_LIB=$PWD/raytrace_amd/_lib/diag/librt_amd_prof.so timeout -k 10 300 python3 tools/phase_prof.py ${c%%:*} ${c#*:} 2 >> $OUT/phase.jsonl 2>> $OUT/phase.err || { echo "phase $c failed"; tail -5 $OUT/phase.err; exit 1; }
       done ;;
     microbench)  # built from source here, never a committed binary
       make -C tools/microbench all > "$OUT/microbench_build.log" 2>&1 || { echo "microbench build failed"; exit 1; }

@@ -1,7 +1,7 @@
 """Phase profile of the decoupled BVH kernel (diagnostic build: tools/build_variant.sh prof
 -DRT_PHASE_PROF): per-wave shader clocks in the front end (items / camera / segment start), the
 traversal rounds and shading, and the lane occupancy of each, for one config and precision.
-usage: RT_AMD_EXPERIMENTS=1 RT_AMD_LIB=raytrace_amd/_lib/exp/librt_amd_prof.so python tools/phase_prof.py CONFIG [f32|f64] [frames]"""
+usage: RT_AMD_EXPERIMENTS=1 RT_AMD_LIB=raytrace_amd/_lib/diag/librt_amd_prof.so python tools/phase_prof.py CONFIG [f32|f64] [frames]"""
 import ctypes
 import json
 import os
@@ -17,7 +17,8 @@ from raytrace_amd.camera import image_height  # noqa: E402
 from raytrace_amd.ray import DeviceScene  # noqa: E402
 
 NAMES = ["front_clk", "trav_clk", "shade_clk", "iters", "rounds", "tracing_lanes", "live_lanes", "shading_lanes",
-         "front_lanes", "node_steps", "node_lanes", "leaf_steps", "leaf_lanes", "node_clk", "leaf_clk"]
+         "front_lanes", "node_steps", "node_lanes", "leaf_steps", "leaf_lanes", "node_clk", "leaf_clk", "cam_clk",
+         "cam_lanes"]
 
 if __name__ == "__main__":
     cfg = sys.argv[1] if len(sys.argv) > 1 else "bunny_cornell"
@@ -40,9 +41,12 @@ if __name__ == "__main__":
     torch.cuda.synchronize()
     n = L.rt_prof_read(1 if prec == "f64" else 0, buf, 32)
     d = dict(zip(NAMES, [buf[i] / frames for i in range(n)]))
-    clk = d["front_clk"] + d["trav_clk"] + d["shade_clk"]
+    # flat kernel (lane_loop_lockstep): front = commit / grab / item, cam = camera ray, trav = the
+    # closest-hit tests of the segment, shade = material, scatter and the sample's sums
+    clk = d["front_clk"] + d["trav_clk"] + d["shade_clk"] + d.get("cam_clk", 0)
     r = {"config": cfg, "precision": prec, "ms_per_frame": ev0.elapsed_time(ev1) / frames,
-         "share": {k: round(d[k] / clk, 4) for k in ("front_clk", "trav_clk", "shade_clk")},
+         "share": {k: round(d.get(k, 0) / clk, 4) for k in ("front_clk", "cam_clk", "trav_clk", "shade_clk")},
+         "cam_lanes_per_iter": round(d.get("cam_lanes", 0) / max(1, d["iters"]), 2),
          "lanes_tracing_per_round": round(d["tracing_lanes"] / max(1, d["rounds"]), 2),
          "lanes_live_per_round": round(d["live_lanes"] / max(1, d["rounds"]), 2),
          "rounds_per_iter": round(d["rounds"] / max(1, d["iters"]), 3),
