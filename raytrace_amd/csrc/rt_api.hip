@@ -151,6 +151,7 @@ struct rt_multi_scene {
   uint8_t* d_codes = nullptr;              // first device: the 8-bit epilogue's output
   size_t codes_cap = 0;
   hipStream_t st0 = nullptr;               // first device: epilogue and device-to-host copy
+  int* h_status = nullptr;                 // pinned host word: the one-device render's status read-back
 };
 
 namespace {
@@ -410,7 +411,8 @@ int multi_create(const std::shared_ptr<const HostScene>& H, const int32_t* devic
       return fail(RT_E_HIP, "stream / events on device %d", devices[k]);
     }
   }
-  if (hipSetDevice(devices[0]) != hipSuccess || hipStreamCreateWithFlags(&M->st0, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(devices[0]) != hipSuccess || hipStreamCreateWithFlags(&M->st0, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc((void**)&M->h_status, 64, hipHostMallocDefault) != hipSuccess) {
     multi_destroy(M);
     return fail(RT_E_HIP, "stream on device %d", devices[0]);
   }
@@ -446,6 +448,7 @@ void multi_destroy(rt_multi_scene* M) {
   if (!M->devices.empty()) {
     (void)hipSetDevice(M->devices[0]);
     if (M->st0) (void)hipStreamDestroy(M->st0);
+    if (M->h_status) (void)hipHostFree(M->h_status);
     (void)hipFree(M->d_gather);
     (void)hipFree(M->d_codes);
   }
@@ -462,6 +465,61 @@ int grow(void** p, size_t* cap, size_t need, int* allocs) {
   HIP_TRY(hipMalloc(p, need ? need : 16));
   *cap = need;
   ++*allocs;
+  return RT_OK;
+}
+
+// One device (the drop-in's plain rt_render / a one-device scene): everything on the part's
+// stream with ONE host synchronisation — status reset, workspace memset, render, resolve, the 8-bit
+// epilogue, the image's device-to-host copy and the status word's into pinned memory — instead of a
+// thread per shard and a synchronising call for each step (the multi-device path below)
+int render_one(rt_multi_scene* M, const rt_camera_settings* cs, uint64_t seed, const rt_exec& ex, int encoding,
+               void* out_host, rt_stats* stats, double build_ms, int allocs,
+               std::chrono::steady_clock::time_point t0) {
+  MultiPart& q = M->parts[0];
+  const rt_device_scene* s = M->scenes[0];
+  const bool f32 = exec_f32(&ex);
+  const int h = rt_host_image_height(cs);
+  const int rows = rt_host_shard_rows(h, &ex);
+  const size_t esize = f32 ? sizeof(float) : sizeof(double);
+  const size_t tile_pixels = (size_t)rows * cs->image_width;
+  HIP_TRY(hipSetDevice(s->device));
+  auto tp = std::chrono::steady_clock::now();
+  if (int r = ensure_precisions(s, f32 ? 1 : 2)) return r;
+  const double prep_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp).count();
+  if (int r = grow(&q.d_tile, &q.tile_cap, tile_pixels * 3 * esize, &allocs)) return r;
+  const size_t wsb = workspace_bytes(tile_pixels, f32 ? RT_ACC_WORDS(float) : RT_ACC_WORDS(double), nullptr, nullptr);
+  if (int r = grow((void**)&q.ws, &q.ws_cap, wsb, &allocs)) return r;
+  HIP_TRY(hipMemsetAsync(s->status, 0, 4 * sizeof(int), q.st));
+  HIP_TRY(hipEventRecord(q.e0, q.st));
+  const int r = f32 ? render_async<float>(s, cs, seed, &ex, (float*)q.d_tile, q.st, q.ws, q.ws_cap, 0)
+                    : render_async<double>(s, cs, seed, &ex, (double*)q.d_tile, q.st, q.ws, q.ws_cap, 0);
+  if (r) return r;
+  HIP_TRY(hipEventRecord(q.e1, q.st));
+  const void* src = q.d_tile;
+  size_t bytes = tile_pixels * 3 * esize;
+  if (encoding >= 0) {
+    const int64_t nv = (int64_t)tile_pixels * 3;
+    if (rt_launch_encode8(q.d_tile, f32 ? 0 : 1, M->d_codes, nv, encode8_table(encoding), encoding, q.st))
+      return fail(RT_E_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
+    src = M->d_codes;
+    bytes = (size_t)nv;
+  }
+  HIP_TRY(hipMemcpyAsync(out_host, src, bytes, hipMemcpyDeviceToHost, q.st));
+  HIP_TRY(hipMemcpyAsync(M->h_status, s->status, sizeof(int), hipMemcpyDeviceToHost, q.st));
+  HIP_TRY(hipStreamSynchronize(q.st));
+  if (*M->h_status) return fail(RT_E_STACK, "BVH traversal stack overflow");
+  if (stats) {
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, q.e0, q.e1));
+    std::memset(stats, 0, sizeof *stats);
+    stats->upload_ms = build_ms + M->upload_ms + prep_ms;
+    stats->kernel_ms = ms;
+    stats->samples = (int64_t)rows * cs->image_width * cs->samples_per_pixel;
+    stats->bvh_nodes = s->n_nodes;
+    stats->max_stack = s->max_depth;
+    stats->device_allocs = allocs;
+    stats->total_ms = build_ms + std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
   return RT_OK;
 }
 
@@ -527,6 +585,7 @@ int multi_render(rt_multi_scene* M, const rt_camera_settings* cs, uint64_t seed,
   if (!rc && n > 1) rc = grow(&M->d_gather, &M->gather_cap, gather_rows * row_bytes, &allocs);
   if (!rc && encoding >= 0)
     rc = grow((void**)&M->d_codes, &M->codes_cap, std::max<size_t>(16, gather_rows * cs->image_width * 3), &allocs);
+  if (!rc && n == 1) return render_one(M, cs, seed, jobs[0].ex, encoding, out_host, stats, build_ms, allocs, t0);
   // a stack overflow of an earlier render must not fail this one: clear each device's status word
   for (size_t j = 0; j < M->scenes.size() && !rc; ++j) {
     const rt_device_scene* s = M->scenes[j];

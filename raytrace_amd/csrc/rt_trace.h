@@ -185,6 +185,8 @@ __device__ __forceinline__ double sqrt_nonneg(double x) {
 // table (rt_sincos_table.h, 2 KB, L1-resident), sin / cos (2 pi b) by short Taylor polynomials
 // (|2 pi b| <= 0.0246: truncation < 1e-17), combined by the angle-addition formulas
 __device__ const double rt_sincos_tab[2 * RT_SINCOS_TABLE_N] = RT_SINCOS_TABLE_INIT;
+// (a table-free version — quadrant reduction and fdlibm's minimax kernels, 3.25 ulp — ran Cornell
+// 4.89 -> 5.42 ms: the table's two loads cost less than the longer polynomials; profiles/r5/variants)
 __device__ __forceinline__ void sincos_turns(double u, double* sn, double* cs) {
   const double kq = __builtin_rint(u * (double)RT_SINCOS_TABLE_N);
   const double b = __builtin_fma(kq, -1.0 / RT_SINCOS_TABLE_N, u);
@@ -925,6 +927,8 @@ RT_FN void acc_add(Acc& A, int c, real x, bool& bad) {
     bad = true;
     return;
   }
+  // (the same words from 32-bit conversions only, floor(x) 2^32 + floor(frac(x) 2^32), measured no
+  // faster: Cornell 4.887 vs 4.889 ms, pawn+fog +1 %; profiles/r5/variants)
   const real xs = x * RL(4294967296.0);
   const real fl = RFLOOR(xs);
   A.hi[c] += (long long)fl;
@@ -1208,16 +1212,18 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
     RT_PROF_PADD(PF_LEAF_LANES, RT_BALLOT_COUNT(true));
     const int enc = ~S.leaf;
     const int first = enc >> RT_LEAF_SHIFT, count = (enc & ((1 << RT_LEAF_SHIFT) - 1)) + 1;
-    for (int k = 0; k < count; ++k)
-    {
-      const PrimRec r = ld_rec(cf(P.prims) + 16 * (size_t)(first + k));
+    auto test_one = [&](const PrimRec& r, int pi) {
       if constexpr (kLeaf == 1)  // every leaf a static triangle (RT_VAR_LEAF_TRI)
-        test_static<RT_PRIM_CLASS_TRI, false>(r, R, S.tmin, S.tmin_up, S.C, first + k);
+        test_static<RT_PRIM_CLASS_TRI, false>(r, R, S.tmin, S.tmin_up, S.C, pi);
       else if constexpr (kLeaf == 2)  // every leaf a static sphere (RT_VAR_LEAF_SPHERE)
-        test_static<RT_PRIM_CLASS_SPHERE, false>(r, R, S.tmin, S.tmin_up, S.C, first + k);
+        test_static<RT_PRIM_CLASS_SPHERE, false>(r, R, S.tmin, S.tmin_up, S.C, pi);
       else
-        test_rec<false, kInst>(P, r, first + k, R, S.tmin, S.tmin_up, S.C, S.inst, S.ord_base);
-    }
+        test_rec<false, kInst>(P, r, pi, R, S.tmin, S.tmin_up, S.C, S.inst, S.ord_base);
+    };
+    // (both records of a 2-record leaf loaded before either test — one memory latency per leaf
+    // instead of two — spilled the binary64 bunny kernel: +3.4 %, pawn+fog FP32 +4 %, demo1 -0.7 %;
+    // profiles/r5/variants)
+    for (int k = 0; k < count; ++k) test_one(ld_rec(cf(P.prims) + 16 * (size_t)(first + k)), first + k);
     S.leaf = 0;
     if (S.node < 0 && S.node != kDone) {  // the node we stopped at is a leaf too: test it next
       S.leaf = S.node;
