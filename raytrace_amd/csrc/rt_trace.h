@@ -1333,38 +1333,51 @@ RT_FN void filt_box(const RT_CAS DevBoxT<float>* B, ff3 o, ff3 d, float ro, floa
   const float tn = fmaxf(fmaxf(lo[0], lo[1]), lo[2]), tf = fminf(fminf(hi[0], hi[1]), hi[2]);
   const int an = lo[0] == tn ? 0 : lo[1] == tn ? 1 : 2, af = hi[0] == tf ? 0 : hi[1] == tf ? 1 : 2;
   const float en = an == 0 ? el[0] : an == 1 ? el[1] : el[2], ef = af == 0 ? eh[0] : af == 1 ? eh[1] : eh[2];
+  if (!(en < 1e30f && ef < 1e30f)) {  // a slab parallel to the ray (or worse): undecided
+    filt_amb(F, -__builtin_huge_valf());
+    return;
+  }
   const float gap = tf - tn, eg = en + ef;
-  // the entry face (the exit face when the entry is surely behind the ray, absent or the face the
-  // ray leaves): certain, undecided (its face known) or ambiguous (a lower bound on t); branch-free
-  // (selects, one update of each kind): the lanes of a wave take different cases
-  const int fn = 2 * an + (an == 0 ? flip[0] : an == 1 ? flip[1] : flip[2]);
+  if (gap < -eg) return;  // the line misses the box
+  bool present;
+  if (tn >= tmin - en) {  // the entry is not surely behind the ray
+    // which face: another slab's entry within the bounds of this one
+    const int close = (lo[0] + el[0] >= tn - en) + (lo[1] + el[1] >= tn - en) + (lo[2] + el[2] >= tn - en);
+    if (close > 1) {
+      filt_amb(F, tn - en);
+      return;
+    }
+    const int fn = 2 * an + (an == 0 ? flip[0] : an == 1 ? flip[1] : flip[2]);
+    const int gid = box_field(B->gid_base, B->gid_code, fn, present);
+    if (present && gid != R.self_gid) {
+      if (gap > eg && tn > tmin + en)
+        filt_add(F, tn, en, box_field(B->prim_base, B->prim_code, fn, present));
+      else  // near the box's edge or tmin: if the entry fails, the exit may win
+        filt_amb(F, tn - en);
+      return;
+    }
+  }
+  if (tf < tmin - ef) return;  // the exit is behind the ray too
+  const int close = (hi[0] - eh[0] <= tf + ef) + (hi[1] - eh[1] <= tf + ef) + (hi[2] - eh[2] <= tf + ef);
+  if (close > 1) {
+    filt_amb(F, tf - ef);
+    return;
+  }
   const int ff = 2 * af + 1 - (af == 0 ? flip[0] : af == 1 ? flip[1] : flip[2]);
-  bool pn, pf;
-  const bool okn = box_field(B->gid_base, B->gid_code, fn, pn) != R.self_gid && pn;
-  const bool okf = box_field(B->gid_base, B->gid_code, ff, pf) != R.self_gid && pf;
-  const int close_n = (lo[0] + el[0] >= tn - en) + (lo[1] + el[1] >= tn - en) + (lo[2] + el[2] >= tn - en);
-  const int close_f = (hi[0] - eh[0] <= tf + ef) + (hi[1] - eh[1] <= tf + ef) + (hi[2] - eh[2] <= tf + ef);
-  const bool wild = !(en < 1e30f && ef < 1e30f);  // a slab parallel to the ray (or worse)
-  const bool meets = !(gap < -eg);                // the line may meet the box
-  const bool entry = meets && tn >= tmin - en;    // the entry is not surely behind the ray
-  const bool entry_amb = entry && (close_n > 1 || (okn && !(gap > eg && tn > tmin + en)));
-  const bool entry_add = entry && close_n <= 1 && okn && gap > eg && tn > tmin + en;
-  const bool to_exit = meets && !(entry && (close_n > 1 || okn)) && tf >= tmin - ef;
-  const bool exit_amb = to_exit && close_f > 1;
-  const bool exit_face = to_exit && close_f <= 1 && okf;
-  const bool exit_add = exit_face && gap > eg && tf > tmin + ef;
-  bool p;
-  const int prim = box_field(B->prim_base, B->prim_code, entry_add ? fn : ff, p);
-  const float inff = __builtin_huge_valf();
-  filt_add(F, entry_add ? tn : exit_add ? tf : inff, entry_add ? en : ef, prim);
-  filt_undecided(F, exit_face && !exit_add ? tf : inff, ef, prim);
-  filt_amb(F, wild ? -inff : entry_amb ? tn - en : exit_amb ? tf - ef : inff);
+  const int gid = box_field(B->gid_base, B->gid_code, ff, present);
+  if (!present || gid == R.self_gid) return;
+  const int prim = box_field(B->prim_base, B->prim_code, ff, present);
+  if (gap > eg && tf > tmin + ef)
+    filt_add(F, tf, ef, prim);
+  else
+    filt_undecided(F, tf, ef, prim);
 }
 // A static parallelogram (kQuad) or triangle in FP32 (record: rt_internal.h prims layout, float)
 template <bool kQuad>
 RT_FN void filt_plane(const RT_CAS float* r, int pi, ff3 o, ff3 d, float ro, float tmin, const RayCtx& R, float W,
                       float Q, FiltBest& F) {
   RT_COUNT(1);
+  if (RT_F2I(r[7]) == R.self_gid) return;
   const ff3 n = {r[0], r[1], r[2]}, qo = {r[4] - o.x, r[5] - o.y, r[6] - o.z};
   const float denom = ffdot(n, d);
   const float inv = RT_RCPF(denom);
@@ -1375,15 +1388,15 @@ RT_FN void filt_plane(const RT_CAS float* r, int pi, ff3 o, ff3 d, float ro, flo
   const float rq = ro + Q;
   const float et = fmaf(rq * 0x1p-20f, fabsf(inv), fabsf(t) * 0x1p-21f);
   const float eab = (kQuad ? 1.f : 2.f) * W * fmaf(fabsf(t) + rq, 0x1p-21f, et);
-  // grazing (|n . d| within the bound of 1e-8) or wild: ambiguous; the face the ray leaves: none
-  const bool self = RT_F2I(r[7]) == R.self_gid;
-  const bool wild = !self && (!(et < 1e30f) || fabsf(denom) <= 0x1p-19f);
-  const bool cand = !self && !wild && !(m1 < -eab || t < tmin - et);
-  const bool sure = cand && m1 > eab && t > tmin + et;
-  const float inff = __builtin_huge_valf();
-  filt_add(F, sure ? t : inff, et, pi);
-  filt_undecided(F, cand && !sure ? t : inff, et, pi);
-  filt_amb(F, wild ? -inff : inff);
+  if (!(et < 1e30f) || fabsf(denom) <= 0x1p-19f) {  // grazing: |n . d| within the bound of 1e-8
+    filt_amb(F, -__builtin_huge_valf());
+    return;
+  }
+  if (m1 < -eab || t < tmin - et) return;
+  if (m1 > eab && t > tmin + et)
+    filt_add(F, t, et, pi);
+  else
+    filt_undecided(F, t, et, pi);
 }
 // The set's per-face binary64 closest hit (every box face by its own record): the lanes the
 // filter leaves undecided.  Flat sets (kPrefix = false): key-only, the winner's primitive is its
