@@ -171,13 +171,8 @@ int ensure_precision(const rt_device_scene* s) {
   HIP_TRY(hipSetDevice(s->device));
   DevArrays<R>& A = s->arrays<R>();
   int rc = A.upload(s->host->arrays<R>());
-  // the binary64 kernels' FP32 closest-hit filter: flat scenes' FP32 flat_recs, or the BVH scenes'
-  // FP32 prims when their surface prefix is filtered (rt_trace.h closest_filtered)
-  const bool flat = (s->variant & RT_VAR_BASE) == RT_VAR_FLAT;
-  const bool prefix_filt = !flat && !(s->variant & RT_VAR_INST) && s->flat_sets[0].filt_ok &&
-                           (s->flat_sets[0].end > s->flat_sets[0].first || s->flat_sets[0].box_end > s->flat_sets[0].box_first);
-  if (!rc && sizeof(R) == 8 && (flat || prefix_filt) &&
-      ((rc = upload(&A.flat_recs32, flat ? s->host->f32.flat_recs : s->host->f32.prims)) == RT_OK))
+  if (!rc && sizeof(R) == 8 && (s->variant & RT_VAR_BASE) == RT_VAR_FLAT &&
+      ((rc = upload(&A.flat_recs32, s->host->f32.flat_recs)) == RT_OK))
     rc = upload(&A.boxes32, s->host->f32.boxes);
   if (rc) {
     A.release();

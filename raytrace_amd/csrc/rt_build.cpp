@@ -822,22 +822,20 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   fill_records(sc, order, slot_of, S.flat, boxes, box_codes, S.prim_mat, S.f64);
   // the binary64 flat kernel's FP32 filter (rt_trace.h closest_filtered): sets of box groups,
   // static parallelograms and triangles, with the scales of their plane records' error bounds
-  // (flat scenes: every set, test-ordered in flat_recs; BVH scenes: the surface prefix, set 0, in
-  // prims)
-  const int n_filt = S.flat ? n_sets : !prefix.empty() ? 1 : 0;
-  for (int s = 0; s < n_filt; ++s) {
-    DevFlatSet& F = S.flat_sets[s];
-    F.filt_ok = F.end_sphere == F.end_tri && F.end == F.end_sphere;
-    double w = 0, q = 0;
-    for (int j = F.first; j < F.end_tri; ++j) {
-      const double* f = (S.flat ? S.f64.flat_recs : S.f64.prims).data() + 16 * (size_t)j;
-      w = std::max(w, std::max(std::fabs(f[8]) + std::fabs(f[9]) + std::fabs(f[10]),
-                               std::fabs(f[12]) + std::fabs(f[13]) + std::fabs(f[14])));
-      q = std::max(q, std::max(std::fabs(f[4]), std::max(std::fabs(f[5]), std::fabs(f[6]))));
+  if (S.flat)
+    for (int s = 0; s < n_sets; ++s) {
+      DevFlatSet& F = S.flat_sets[s];
+      F.filt_ok = F.end_sphere == F.end_tri && F.end == F.end_sphere;
+      double w = 0, q = 0;
+      for (int j = F.first; j < F.end_tri; ++j) {
+        const double* f = S.f64.flat_recs.data() + 16 * (size_t)j;
+        w = std::max(w, std::max(std::fabs(f[8]) + std::fabs(f[9]) + std::fabs(f[10]),
+                                 std::fabs(f[12]) + std::fabs(f[13]) + std::fabs(f[14])));
+        q = std::max(q, std::max(std::fabs(f[4]), std::max(std::fabs(f[5]), std::fabs(f[6]))));
+      }
+      F.filt_w = (float)(w * (1 + 1e-6));
+      F.filt_q = (float)(q * (1 + 1e-6));
     }
-    F.filt_w = (float)(w * (1 + 1e-6));
-    F.filt_q = (float)(q * (1 + 1e-6));
-  }
   fill_instances(sc, blas_root, S.f32);
   fill_instances(sc, blas_root, S.f64);
   S.n_instances = sc->n_instances;

@@ -738,24 +738,10 @@ RT_FN void test_box(const RT_CAS DevBox* B, const RayCtx& R, real tmin_up, Close
 // BVH scenes: the surface set's large-primitive prefix (rt_build.cpp; P.flat_sets[0]), tested
 // before the traversal so that its closest hit bounds it.  The range is a kernel argument, so
 // the records are wave-uniform (scalar loads) even when only some lanes start a query here.
-#ifndef RT_FLAT_FILTER
-#define RT_FLAT_FILTER 1
-#endif
-#if RT_F64 && RT_FLAT_FILTER
-template <bool kPrefix>
-RT_FN void closest_filtered(const KernelParams& P, const DevFlatSet& S, const RayCtx& R, real tmin, Closest& C);
-#endif
 template <bool kInst = false>
 RT_FN void prefix_hits(const KernelParams& P, cfp prims, const RayCtx& R, real tmin, Closest& C) {
   const DevFlatSet& S = P.flat_sets[0];
   if (!P.surface_prefix || (S.end == S.first && S.box_end == S.box_first)) return;
-#if RT_F64 && RT_FLAT_FILTER
-  // binary64 kernels: the prefix through the FP32 filter (closest_filtered), as a flat set
-  if (!kInst && P.flat_filter && S.filt_ok) {
-    closest_filtered<true>(P, S, R, tmin, C);
-    return;
-  }
-#endif
   const real tmin_up = float_up(tmin);
   for (int b = S.box_first; b < S.box_end; ++b)
     test_box<false, kInst>((const RT_CAS DevBox*)P.boxes + b, R, tmin_up, C);
@@ -1263,6 +1249,9 @@ RT_FN void test_leaf_generic(const KernelParams& P, RC& R, TravState& S) {
   }
 }
 
+#ifndef RT_FLAT_FILTER
+#define RT_FLAT_FILTER 1
+#endif
 #if RT_F64
 // ---------------------------------------------------------------- FP32 filter (flat binary64 kernel)
 // The binary64 flat kernel's closest hit, per segment: every record of the set is tested in FP32
@@ -1374,7 +1363,7 @@ RT_FN void filt_box(const RT_CAS DevBoxT<float>* B, ff3 o, ff3 d, float ro, floa
 }
 // A static parallelogram (kQuad) or triangle in FP32 (record: rt_internal.h prims layout, float)
 template <bool kQuad>
-RT_FN void filt_plane(const RT_CAS float* r, int pi, ff3 o, ff3 d, float ro, float tmin, const RayCtx& R, float W,
+RT_FN void filt_plane(const RT_CAS float* r, ff3 o, ff3 d, float ro, float tmin, const RayCtx& R, float W,
                       float Q, FiltBest& F) {
   RT_COUNT(1);
   if (RT_F2I(r[7]) == R.self_gid) return;
@@ -1394,15 +1383,12 @@ RT_FN void filt_plane(const RT_CAS float* r, int pi, ff3 o, ff3 d, float ro, flo
   }
   if (m1 < -eab || t < tmin - et) return;
   if (m1 > eab && t > tmin + et)
-    filt_add(F, t, et, pi);
+    filt_add(F, t, et, RT_F2I(r[11]));
   else
-    filt_undecided(F, t, et, pi);
+    filt_undecided(F, t, et, RT_F2I(r[11]));
 }
 // The set's per-face binary64 closest hit (every box face by its own record): the lanes the
-// filter leaves undecided.  Flat sets (kPrefix = false): key-only, the winner's primitive is its
-// slot, the records test-ordered in flat_recs; the BVH scenes' surface prefix (kPrefix): records
-// in prims, keyed by their depth-first order
-template <bool kPrefix>
+// filter leaves undecided; key-only, the winner's primitive is its slot
 RT_FN void closest_exact_faces(const KernelParams& P, const DevFlatSet& S, const RayCtx& R, real tmin, Closest& C) {
   const real tmin_up = float_up(tmin);
   for (int b = S.box_first; b < S.box_end; ++b) {
@@ -1410,20 +1396,15 @@ RT_FN void closest_exact_faces(const KernelParams& P, const DevFlatSet& S, const
     for (int f = 0; f < 6; ++f) {
       bool present;
       const int pi = box_field(B->prim_base, B->prim_code, f, present);
-      if (present)
-        test_static<RT_PRIM_CLASS_QUAD, !kPrefix>(ld_rec64((const RT_CAS PrimRec64*)P.prims + pi), R, tmin, tmin_up, C, pi);
+      if (present) test_static<RT_PRIM_CLASS_QUAD>(ld_rec64((const RT_CAS PrimRec64*)P.prims + pi), R, tmin, tmin_up, C);
     }
   }
   int k = S.first;
-  const RT_CAS PrimRec64* rp = (const RT_CAS PrimRec64*)(kPrefix ? P.prims : P.flat_recs) + k;
-  for (; k < S.end_quad; ++k, ++rp) test_static<RT_PRIM_CLASS_QUAD, !kPrefix>(ld_rec64(rp), R, tmin, tmin_up, C, k);
-  for (; k < S.end_tri; ++k, ++rp) test_static<RT_PRIM_CLASS_TRI, !kPrefix>(ld_rec64(rp), R, tmin, tmin_up, C, k);
-  if (!kPrefix && C.t < kInf) C.prim = C.ord;
+  const RT_CAS PrimRec64* rp = (const RT_CAS PrimRec64*)P.flat_recs + k;
+  for (; k < S.end_quad; ++k, ++rp) test_static<RT_PRIM_CLASS_QUAD>(ld_rec64(rp), R, tmin, tmin_up, C);
+  for (; k < S.end_tri; ++k, ++rp) test_static<RT_PRIM_CLASS_TRI>(ld_rec64(rp), R, tmin, tmin_up, C);
+  if (C.t < kInf) C.prim = C.ord;
 }
-// P.flat_recs32 holds the set's FP32 records: flat scenes' test-ordered flat_recs, or the BVH
-// scenes' prims (kPrefix); a flat record's primitive is its slot (its order word), a prefix
-// record's its index
-template <bool kPrefix>
 RT_FN void closest_filtered(const KernelParams& P, const DevFlatSet& S, const RayCtx& R, real tmin, Closest& C) {
   const ff3 o = {(float)R.o.x, (float)R.o.y, (float)R.o.z}, d = {(float)R.d.x, (float)R.d.y, (float)R.d.z};
   const float ro = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
@@ -1433,10 +1414,8 @@ RT_FN void closest_filtered(const KernelParams& P, const DevFlatSet& S, const Ra
   for (int b = S.box_first; b < S.box_end; ++b) filt_box((const RT_CAS DevBoxT<float>*)P.boxes32 + b, o, d, ro, tm, R, F);
   int k = S.first;
   const RT_CAS float* rp = (const RT_CAS float*)P.flat_recs32 + 16 * k;
-  for (; k < S.end_quad; ++k, rp += 16)
-    filt_plane<true>(rp, kPrefix ? k : RT_F2I(rp[11]), o, d, ro, tm, R, S.filt_w, S.filt_q, F);
-  for (; k < S.end_tri; ++k, rp += 16)
-    filt_plane<false>(rp, kPrefix ? k : RT_F2I(rp[11]), o, d, ro, tm, R, S.filt_w, S.filt_q, F);
+  for (; k < S.end_quad; ++k, rp += 16) filt_plane<true>(rp, o, d, ro, tm, R, S.filt_w, S.filt_q, F);
+  for (; k < S.end_tri; ++k, rp += 16) filt_plane<false>(rp, o, d, ro, tm, R, S.filt_w, S.filt_q, F);
   // binary64 tests of B and, when it could beat B, of A, each by its own record (a box face is a
   // parallelogram), the fields the plane test reads only
   const bool test_a = F.aprim >= 0 && F.at - F.ae <= F.t + F.e;
@@ -1461,7 +1440,7 @@ RT_FN void closest_filtered(const KernelParams& P, const DevFlatSet& S, const Ra
     if (undecided) {
       RT_COUNT(4);
       C = no_hit();
-      closest_exact_faces<kPrefix>(P, S, R, tmin, C);
+      closest_exact_faces(P, S, R, tmin, C);
     }
 }
 #endif
@@ -1477,7 +1456,7 @@ RT_FN_SPEC void closest<true>(const KernelParams& P, cfp prims, int root, int se
   (void)overflow;
 #if RT_F64 && RT_FLAT_FILTER
   if (P.flat_filter && P.flat_sets[set].filt_ok) {
-    closest_filtered<false>(P, P.flat_sets[set], R, tmin, C);
+    closest_filtered(P, P.flat_sets[set], R, tmin, C);
     return;
   }
 #endif

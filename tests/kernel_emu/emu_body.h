@@ -102,9 +102,9 @@ int render(const HostScene& H, const rt_camera_settings* cs, uint64_t seed, cons
   P.boxes = A.boxes.data();
   P.instances = A.instances.data();
   // the binary64 flat kernel's FP32 filter, as rt_api.hip render_async sets it
-  P.flat_recs32 = (H.flat ? H.f32.flat_recs : H.f32.prims).data();
+  P.flat_recs32 = H.f32.flat_recs.data();
   P.boxes32 = H.f32.boxes.data();
-  P.flat_filter = RT_F64 && (H.flat || (H.n_instances == 0 && H.flat_sets[0].filt_ok));
+  P.flat_filter = RT_F64 && H.flat;
   if (const char* e = rt_knob("RT_AMD_FLAT_FILTER")) P.flat_filter = P.flat_filter && atoi(e) != 0;
   P.out = out;
   P.surface_root = H.surface_root;
