@@ -65,10 +65,6 @@ struct DevArrays {
   R* flat_recs = nullptr;
   DevBoxT<R>* boxes = nullptr;
   DevInstanceT<R>* instances = nullptr;
-  // binary64 flat scenes: the FP32 copies of flat_recs and boxes for the kernel's closest-hit
-  // filter (KernelParams::flat_recs32 / boxes32)
-  float* flat_recs32 = nullptr;
-  DevBoxT<float>* boxes32 = nullptr;
   DevMediumT<R> media[RT_MAX_MEDIA];
   int resident_blocks = 0;  // render-kernel workgroups resident on the device (occupancy query)
   int lds_nodes = 0;        // top surface-BVH nodes this precision's kernel stages in LDS per workgroup
@@ -87,7 +83,7 @@ struct DevArrays {
   void release() {
     for (void* p : {(void*)prims, (void*)prim_shade, (void*)prim_uv, (void*)mats, (void*)texs, (void*)motions,
                     (void*)uvframes, (void*)texels, (void*)perlin_grad, (void*)flat_recs, (void*)boxes,
-                    (void*)instances, (void*)flat_recs32, (void*)boxes32})
+                    (void*)instances})
       (void)hipFree(p);
   }
 };
@@ -171,9 +167,6 @@ int ensure_precision(const rt_device_scene* s) {
   HIP_TRY(hipSetDevice(s->device));
   DevArrays<R>& A = s->arrays<R>();
   int rc = A.upload(s->host->arrays<R>());
-  if (!rc && sizeof(R) == 8 && (s->variant & RT_VAR_BASE) == RT_VAR_FLAT &&
-      ((rc = upload(&A.flat_recs32, s->host->f32.flat_recs)) == RT_OK))
-    rc = upload(&A.boxes32, s->host->f32.boxes);
   if (rc) {
     A.release();
     A = DevArrays<R>();
@@ -241,12 +234,6 @@ int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_
   P.flat_recs = A.flat_recs;
   P.boxes = A.boxes;
   P.instances = A.instances;
-  P.flat_recs32 = A.flat_recs32;
-  P.boxes32 = A.boxes32;
-  // the binary64 flat kernel's FP32 closest-hit filter (rt_trace.h closest_filtered); the knob
-  // RT_AMD_FLAT_FILTER=0 tests every record in binary64 (A/B, tests)
-  P.flat_filter = A.flat_recs32 != nullptr;
-  if (const char* e = rt_knob("RT_AMD_FLAT_FILTER")) P.flat_filter = P.flat_filter && atoi(e) != 0;
   P.status = s->status;
   P.out = d_out;
   P.surface_root = s->surface_root;

@@ -225,11 +225,6 @@ void fill_records(const rt_scene* sc, const std::vector<int>& order, const std::
     d.gid_code = codes[b].gid_code;
     d.prim_base = codes[b].prim_base;
     d.prim_code = codes[b].prim_code;
-    double an = 0;
-    for (int k = 0; k < 3; ++k)
-      an = std::max(an, std::fabs(boxes[b].a[k].x) + std::fabs(boxes[b].a[k].y) + std::fabs(boxes[b].a[k].z));
-    d.filt_a = (float)(an * (1 + 1e-6));
-    d.filt_c = (float)(std::max(std::fabs(boxes[b].c.x), std::max(std::fabs(boxes[b].c.y), std::fabs(boxes[b].c.z))) * (1 + 1e-6));
     A.boxes.push_back(d);
   }
   A.prims.assign((size_t)n * 16, (R)0);
@@ -698,6 +693,7 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
       F.end_sphere = F.end_tri + cnt[2];
       F.end = F.end_sphere + cnt[3];
       F.box_first = F.box_end = 0;
+      F.pad = 0;
     }
   }
   // box groups among each flat set's static parallelograms (and the surface prefix): their
@@ -820,22 +816,6 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   }
   fill_records(sc, order, slot_of, S.flat, boxes, box_codes, S.prim_mat, S.f32);
   fill_records(sc, order, slot_of, S.flat, boxes, box_codes, S.prim_mat, S.f64);
-  // the binary64 flat kernel's FP32 filter (rt_trace.h closest_filtered): sets of box groups,
-  // static parallelograms and triangles, with the scales of their plane records' error bounds
-  if (S.flat)
-    for (int s = 0; s < n_sets; ++s) {
-      DevFlatSet& F = S.flat_sets[s];
-      F.filt_ok = F.end_sphere == F.end_tri && F.end == F.end_sphere;
-      double w = 0, q = 0;
-      for (int j = F.first; j < F.end_tri; ++j) {
-        const double* f = S.f64.flat_recs.data() + 16 * (size_t)j;
-        w = std::max(w, std::max(std::fabs(f[8]) + std::fabs(f[9]) + std::fabs(f[10]),
-                                 std::fabs(f[12]) + std::fabs(f[13]) + std::fabs(f[14])));
-        q = std::max(q, std::max(std::fabs(f[4]), std::max(std::fabs(f[5]), std::fabs(f[6]))));
-      }
-      F.filt_w = (float)(w * (1 + 1e-6));
-      F.filt_q = (float)(q * (1 + 1e-6));
-    }
   fill_instances(sc, blas_root, S.f32);
   fill_instances(sc, blas_root, S.f64);
   S.n_instances = sc->n_instances;

@@ -189,12 +189,7 @@ struct DevMediumT {
 struct DevFlatSet {
   int first, end_quad, end_tri, end_sphere, end;
   int box_first, box_end;  // its box groups: KernelParams::boxes[box_first, box_end)
-  // the binary64 flat kernel's FP32 filter (rt_trace.h closest_filtered): the set holds only box
-  // groups, static parallelograms and triangles (filt_ok), and the scales of its plane records'
-  // error bounds: the largest |wa|_1, |wb|_1 (filt_w) and |q|_inf (filt_q)
-  int filt_ok;
-  float filt_w, filt_q;
-  int pad[2];
+  int pad;
 };
 
 // Box groups.  Parallelograms of one flat set (or of the BVH scenes' surface prefix) that are
@@ -219,8 +214,7 @@ struct DevBoxT {
   int gid_code;
   int prim_base;   // primitive index of the faces
   int prim_code;
-  // the FP32 filter's error scales (rt_trace.h filt_box): max_k |a_k|_1 and |c|_inf
-  float filt_a, filt_c;
+  int pad[2];
 };
 
 template <class R>
@@ -281,11 +275,6 @@ struct KernelParamsT {
   const R* flat_recs;      // flat scenes: the test records, class-grouped (DevFlatSet ranges)
   const DevBoxT<R>* boxes; // box groups of the flat sets / the surface prefix (DevBox)
   const DevInstanceT<R>* instances;  // two-level instancing (RT_VAR_INST)
-  // binary64 flat kernel: FP32 copies of flat_recs and boxes for its closest-hit filter
-  // (rt_trace.h closest_filtered; flat_filter = 0: every record tested in binary64)
-  const float* flat_recs32;
-  const DevBoxT<float>* boxes32;
-  int flat_filter;
   R* out;                  // linear RGB of the tile, R per channel
   int* status;             // device word: nonzero on stack overflow
   // persistent-lane work queue (rt_trace.h lane_loop): items = n_chunks x tile pixels

@@ -18,11 +18,7 @@
 #ifndef RT_ACC_IN_LDS
 #define RT_ACC_IN_LDS 1
 #endif
-#ifndef RT_ACC_LDS_FLAT64
-#define RT_ACC_LDS_FLAT64 0
-#endif
-#define RT_ACC_LDS_OF(kVar, kMedia) \
-  (RT_ACC_IN_LDS && ((kVar) != RT_VAR_FLAT || (RT_F64 && RT_ACC_LDS_FLAT64)) && (RT_F64 || !(kMedia)))
+#define RT_ACC_LDS_OF(kVar, kMedia) (RT_ACC_IN_LDS && (kVar) != RT_VAR_FLAT && (RT_F64 || !(kMedia)))
 
 namespace RT_NS {
 

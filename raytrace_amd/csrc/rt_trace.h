@@ -52,9 +52,8 @@ inline int f2i(float f) {
   std::memcpy(&i, &f, 4);
   return i;
 }
-// traversal counters of the host build (nodes visited, primitives tested, segments, -, lanes the
-// flat binary64 kernel's FP32 filter left undecided)
-extern thread_local long long counters[5];
+// traversal counters of the host build (nodes visited, primitives tested, segments)
+extern thread_local long long counters[4];
 }  // namespace rt_emu
 #define RT_F2I(f) rt_emu::f2i(f)
 #define RT_COUNT(i) (++rt_emu::counters[i])
@@ -1249,202 +1248,6 @@ RT_FN void test_leaf_generic(const KernelParams& P, RC& R, TravState& S) {
   }
 }
 
-#ifndef RT_FLAT_FILTER
-#define RT_FLAT_FILTER 1
-#endif
-#if RT_F64
-// ---------------------------------------------------------------- FP32 filter (flat binary64 kernel)
-// The binary64 flat kernel's closest hit, per segment: every record of the set is tested in FP32
-// (half the issue cost of binary64) with an error bound; only the winner is then tested in
-// binary64, as a parallelogram / triangle — a box group's winning face by its own record.  The
-// result is the closest hit of the per-face binary64 tests (the reference's cuboid is six
-// planeShapes, Geometry.hs:154-166), which the lanes whose FP32 tests cannot decide it (another
-// candidate, or a test within its bound of a threshold, no further than the winner's bound) run
-// in full (closest_exact_faces).  The bounds are conservative for FP32 rounding: box groups in box
-// units, sigma = 2^-20 max_k|a_k|_1 (|o|_inf + |c|_inf) on s_k = a_k . (o - c), and a relative
-// 2^-21 max|a|_1 on a_k . d (rt_build.cpp filt_a / filt_c); planes 2^-20 (|o| + |q|) / |n . d| + 2^-21
-// |t| on t and 2^-21 W (|t| + |o| + |q|) + W dt on the face coordinates (DevFlatSet filt_w /
-// filt_q) — 16x or more the rounding they cover.
-struct FiltBest {
-  float t, e;      // B, the best certain candidate: FP32 t and its bound
-  int prim;        // its primitive = its slot = its key order (flat sets store prims in slot order)
-  float at, ae;    // A, the lowest (t - bound) candidate whose validity the bound cannot decide
-  int aprim;       // its primitive (= slot; -1: none)
-  float lo_other;  // the lowest t - bound of every other candidate, certain or not
-};
-struct ff3 {
-  float x, y, z;
-};
-RT_FN float ffdot(ff3 a, ff3 b) { return fmaf(a.x, b.x, fmaf(a.y, b.y, a.z * b.z)); }
-RT_FN void filt_add(FiltBest& F, float t, float e, int prim) {
-  const bool better = t < F.t || (t == F.t && prim < F.prim);
-  F.lo_other = fminf(F.lo_other, better ? F.t - F.e : t - e);
-  F.t = better ? t : F.t;
-  F.e = better ? e : F.e;
-  F.prim = better ? prim : F.prim;
-}
-RT_FN void filt_amb(FiltBest& F, float tlo) { F.lo_other = fminf(F.lo_other, tlo); }
-// a candidate whose face is known but whose validity is within the bound of its threshold: it is
-// tested in binary64 beside B when it could beat B (the lowest one; the others bound lo_other)
-RT_FN void filt_undecided(FiltBest& F, float t, float e, int prim) {
-  const bool lower = t - e < F.at - F.ae;
-  F.lo_other = fminf(F.lo_other, lower ? F.at - F.ae : t - e);
-  F.at = lower ? t : F.at;
-  F.ae = lower ? e : F.ae;
-  F.aprim = lower ? prim : F.aprim;
-}
-RT_FN float med3f(float a, float b, float c) { return fmaxf(fminf(a, b), fminf(fmaxf(a, b), c)); }
-// A box group in FP32: the entry face (the exit face when the entry is behind the ray, absent or
-// the face the ray leaves) as a certain candidate, or a lower bound on t where it cannot decide
-RT_FN void filt_box(const RT_CAS DevBoxT<float>* B, ff3 o, ff3 d, float ro, float tmin, const RayCtx& R,
-                    FiltBest& F) {
-  RT_COUNT(1);
-  const ff3 oc = {o.x - B->c[0], o.y - B->c[1], o.z - B->c[2]};
-  const ff3 ax[3] = {ff3{B->a0[0], B->a0[1], B->a0[2]}, ff3{B->a1[0], B->a1[1], B->a1[2]},
-                     ff3{B->a2[0], B->a2[1], B->a2[2]}};
-  // per axis: the slab's entry / exit t and their bounds: |ds| <= sig (box units) and
-  // |d(a.d)| <= 2^-21 |a|_1 make t = (s' - s) / (a.d) off by <= (sig + |t| 2^-21 |a|_1) / |a.d|, plus
-  // 2^-22 |t| for the reciprocal and the products
-  const float sig = B->filt_a * (ro + B->filt_c) * 0x1p-20f, ar = B->filt_a * 0x1p-21f;
-  float lo[3], hi[3], el[3], eh[3];
-  int flip[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const float inv = RT_RCPF(ffdot(ax[k], d));
-    const float sk = ffdot(ax[k], oc);
-    const float t0 = -sk * inv, t1 = fmaf(-sk, inv, inv);
-    flip[k] = (int)(__builtin_bit_cast(uint32_t, inv) >> 31);
-    lo[k] = fminf(t0, t1);
-    hi[k] = fmaxf(t0, t1);
-    el[k] = fmaf(fmaf(fabsf(lo[k]), ar, sig), fabsf(inv), fabsf(lo[k]) * 0x1p-22f);
-    eh[k] = fmaf(fmaf(fabsf(hi[k]), ar, sig), fabsf(inv), fabsf(hi[k]) * 0x1p-22f);
-  }
-  const float tn = fmaxf(fmaxf(lo[0], lo[1]), lo[2]), tf = fminf(fminf(hi[0], hi[1]), hi[2]);
-  const int an = lo[0] == tn ? 0 : lo[1] == tn ? 1 : 2, af = hi[0] == tf ? 0 : hi[1] == tf ? 1 : 2;
-  const float en = an == 0 ? el[0] : an == 1 ? el[1] : el[2], ef = af == 0 ? eh[0] : af == 1 ? eh[1] : eh[2];
-  if (!(en < 1e30f && ef < 1e30f)) {  // a slab parallel to the ray (or worse): undecided
-    filt_amb(F, -__builtin_huge_valf());
-    return;
-  }
-  const float gap = tf - tn, eg = en + ef;
-  if (gap < -eg) return;  // the line misses the box
-  bool present;
-  if (tn >= tmin - en) {  // the entry is not surely behind the ray
-    // which face: another slab's entry within the bounds of this one
-    const int close = (lo[0] + el[0] >= tn - en) + (lo[1] + el[1] >= tn - en) + (lo[2] + el[2] >= tn - en);
-    if (close > 1) {
-      filt_amb(F, tn - en);
-      return;
-    }
-    const int fn = 2 * an + (an == 0 ? flip[0] : an == 1 ? flip[1] : flip[2]);
-    const int gid = box_field(B->gid_base, B->gid_code, fn, present);
-    if (present && gid != R.self_gid) {
-      if (gap > eg && tn > tmin + en)
-        filt_add(F, tn, en, box_field(B->prim_base, B->prim_code, fn, present));
-      else  // near the box's edge or tmin: if the entry fails, the exit may win
-        filt_amb(F, tn - en);
-      return;
-    }
-  }
-  if (tf < tmin - ef) return;  // the exit is behind the ray too
-  const int close = (hi[0] - eh[0] <= tf + ef) + (hi[1] - eh[1] <= tf + ef) + (hi[2] - eh[2] <= tf + ef);
-  if (close > 1) {
-    filt_amb(F, tf - ef);
-    return;
-  }
-  const int ff = 2 * af + 1 - (af == 0 ? flip[0] : af == 1 ? flip[1] : flip[2]);
-  const int gid = box_field(B->gid_base, B->gid_code, ff, present);
-  if (!present || gid == R.self_gid) return;
-  const int prim = box_field(B->prim_base, B->prim_code, ff, present);
-  if (gap > eg && tf > tmin + ef)
-    filt_add(F, tf, ef, prim);
-  else
-    filt_undecided(F, tf, ef, prim);
-}
-// A static parallelogram (kQuad) or triangle in FP32 (record: rt_internal.h prims layout, float)
-template <bool kQuad>
-RT_FN void filt_plane(const RT_CAS float* r, ff3 o, ff3 d, float ro, float tmin, const RayCtx& R, float W,
-                      float Q, FiltBest& F) {
-  RT_COUNT(1);
-  if (RT_F2I(r[7]) == R.self_gid) return;
-  const ff3 n = {r[0], r[1], r[2]}, qo = {r[4] - o.x, r[5] - o.y, r[6] - o.z};
-  const float denom = ffdot(n, d);
-  const float inv = RT_RCPF(denom);
-  const float t = ffdot(n, qo) * inv;
-  const ff3 prel = {fmaf(t, d.x, -qo.x), fmaf(t, d.y, -qo.y), fmaf(t, d.z, -qo.z)};
-  const float a = ffdot(prel, ff3{r[8], r[9], r[10]}), b = ffdot(prel, ff3{r[12], r[13], r[14]});
-  const float m1 = kQuad ? fminf(fminf(a, b), fminf(1.f - a, 1.f - b)) : fminf(fminf(a, b), 1.f - a - b);
-  const float rq = ro + Q;
-  const float et = fmaf(rq * 0x1p-20f, fabsf(inv), fabsf(t) * 0x1p-21f);
-  const float eab = (kQuad ? 1.f : 2.f) * W * fmaf(fabsf(t) + rq, 0x1p-21f, et);
-  if (!(et < 1e30f) || fabsf(denom) <= 0x1p-19f) {  // grazing: |n . d| within the bound of 1e-8
-    filt_amb(F, -__builtin_huge_valf());
-    return;
-  }
-  if (m1 < -eab || t < tmin - et) return;
-  if (m1 > eab && t > tmin + et)
-    filt_add(F, t, et, RT_F2I(r[11]));
-  else
-    filt_undecided(F, t, et, RT_F2I(r[11]));
-}
-// The set's per-face binary64 closest hit (every box face by its own record): the lanes the
-// filter leaves undecided; key-only, the winner's primitive is its slot
-RT_FN void closest_exact_faces(const KernelParams& P, const DevFlatSet& S, const RayCtx& R, real tmin, Closest& C) {
-  const real tmin_up = float_up(tmin);
-  for (int b = S.box_first; b < S.box_end; ++b) {
-    const RT_CAS DevBox* B = (const RT_CAS DevBox*)P.boxes + b;
-    for (int f = 0; f < 6; ++f) {
-      bool present;
-      const int pi = box_field(B->prim_base, B->prim_code, f, present);
-      if (present) test_static<RT_PRIM_CLASS_QUAD>(ld_rec64((const RT_CAS PrimRec64*)P.prims + pi), R, tmin, tmin_up, C);
-    }
-  }
-  int k = S.first;
-  const RT_CAS PrimRec64* rp = (const RT_CAS PrimRec64*)P.flat_recs + k;
-  for (; k < S.end_quad; ++k, ++rp) test_static<RT_PRIM_CLASS_QUAD>(ld_rec64(rp), R, tmin, tmin_up, C);
-  for (; k < S.end_tri; ++k, ++rp) test_static<RT_PRIM_CLASS_TRI>(ld_rec64(rp), R, tmin, tmin_up, C);
-  if (C.t < kInf) C.prim = C.ord;
-}
-RT_FN void closest_filtered(const KernelParams& P, const DevFlatSet& S, const RayCtx& R, real tmin, Closest& C) {
-  const ff3 o = {(float)R.o.x, (float)R.o.y, (float)R.o.z}, d = {(float)R.d.x, (float)R.d.y, (float)R.d.z};
-  const float ro = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
-  const float tm = (float)tmin;
-  const float inff = __builtin_huge_valf();
-  FiltBest F{inff, 0.f, -1, inff, 0.f, -1, inff};
-  for (int b = S.box_first; b < S.box_end; ++b) filt_box((const RT_CAS DevBoxT<float>*)P.boxes32 + b, o, d, ro, tm, R, F);
-  int k = S.first;
-  const RT_CAS float* rp = (const RT_CAS float*)P.flat_recs32 + 16 * k;
-  for (; k < S.end_quad; ++k, rp += 16) filt_plane<true>(rp, o, d, ro, tm, R, S.filt_w, S.filt_q, F);
-  for (; k < S.end_tri; ++k, rp += 16) filt_plane<false>(rp, o, d, ro, tm, R, S.filt_w, S.filt_q, F);
-  // binary64 tests of B and, when it could beat B, of A, each by its own record (a box face is a
-  // parallelogram), the fields the plane test reads only
-  const bool test_a = F.aprim >= 0 && F.at - F.ae <= F.t + F.e;
-  const real tmin_up = float_up(tmin);
-  auto exact = [&](int pi) {
-    const real* r = P.prims + 16 * (size_t)pi;
-    const PrimRec rec{v4{r[0], r[1], r[2], r[3]}, v4{r[4], r[5], r[6], r[7]}, v4{r[8], r[9], r[10], r[11]},
-                      v4{r[12], r[13], r[14], RL(0.)}};
-    real t, q;
-    isect_plane<-1>(rec, R.o, R, tmin_up, is_self<false>(R, RT_R2I(rec.b.w), -1), t, q,
-                    (RT_R2I(rec.a.w) & RT_KIND_MASK) == 1);
-    consider<false>(C, t, q, RT_R2I(rec.c.w), pi);
-  };
-  if (F.prim >= 0) exact(F.prim);
-  if (RT_ANY(test_a))
-    if (test_a) exact(F.aprim);
-  // decided: B passed its binary64 test (always, within the bound), and no other candidate comes
-  // within the winner's bound (or there is none at all)
-  const float whi = F.aprim >= 0 && C.prim == F.aprim ? F.at + F.ae : F.t + F.e;
-  bool undecided = (F.prim >= 0 && C.prim < 0) || (F.lo_other <= whi && F.lo_other < inff);
-  if (RT_ANY(undecided))
-    if (undecided) {
-      RT_COUNT(4);
-      C = no_hit();
-      closest_exact_faces(P, S, R, tmin, C);
-    }
-}
-#endif
-
 // kFlat: the set is one flat leaf (rt_internal.h DevFlatSet); every lane walks the same
 // records in the same order, so the loops are coherent and the records are scalar loads.
 template <>
@@ -1454,12 +1257,6 @@ RT_FN_SPEC void closest<true>(const KernelParams& P, cfp prims, int root, int se
   (void)root;
   (void)W;
   (void)overflow;
-#if RT_F64 && RT_FLAT_FILTER
-  if (P.flat_filter && P.flat_sets[set].filt_ok) {
-    closest_filtered(P, P.flat_sets[set], R, tmin, C);
-    return;
-  }
-#endif
   {
     // set comes from the kernel arguments: the ranges are wave-uniform, every loop is scalar
     const DevFlatSet& S = P.flat_sets[set];

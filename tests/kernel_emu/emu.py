@@ -39,7 +39,7 @@ def render(settings, world, seed, n_shards=1, shard=0, row_block=4, nthreads=Non
     rows = shard_rows(h, n_shards, row_block)
     out = np.zeros((rows, int(settings.cs_imageWidth), 3), np.float64 if precision == "f64" else np.float32)
     L = lib()
-    cnt = np.zeros(5, np.int64)
+    cnt = np.zeros(4, np.int64)
     rc = L.rt_emu_render(ctypes.byref(cs), ctypes.byref(sc), ctypes.c_uint64(_seed64(seed)), ctypes.byref(ex),
                          out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(nthreads or min(16, os.cpu_count() or 1)),
                          ctypes.c_int(chunk), cnt.ctypes.data_as(ctypes.c_void_p),
@@ -47,7 +47,7 @@ def render(settings, world, seed, n_shards=1, shard=0, row_block=4, nthreads=Non
     if rc != 0:
         raise RuntimeError(f"rt_emu_render failed {rc}: {L.rt_emu_last_error().decode()}")
     if counters:
-        return out, dict(zip(["bvh_nodes", "prims_tested", "segments", "samples", "filter_undecided"], cnt.tolist()))
+        return out, dict(zip(["bvh_nodes", "prims_tested", "segments", "samples"], cnt.tolist()))
     return out
 
 

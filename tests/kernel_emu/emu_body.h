@@ -8,7 +8,7 @@ struct Shared {
   std::atomic<int> overflow{0};
   std::vector<std::atomic<long long>>* accum;
   std::vector<std::atomic<unsigned>>* flags;
-  std::atomic<long long> cnt[5];
+  std::atomic<long long> cnt[4];
 };
 
 // the device kernel's WaveWork without waves: one shared counter, every item committed directly
@@ -75,7 +75,7 @@ void* worker(void* arg) {
   const RT_NS::Trav W{stack.data(), 1, nullptr};  // the emulator reads every node from memory
   int ov = run_variant(*s->P, s->variant, g, W);
   if (ov) s->overflow = 1;
-  for (int i = 0; i < 5; ++i) s->cnt[i] += rt_emu::counters[i];
+  for (int i = 0; i < 4; ++i) s->cnt[i] += rt_emu::counters[i];
   return nullptr;
 }
 
@@ -101,11 +101,6 @@ int render(const HostScene& H, const rt_camera_settings* cs, uint64_t seed, cons
   P.flat_recs = A.flat_recs.data();
   P.boxes = A.boxes.data();
   P.instances = A.instances.data();
-  // the binary64 flat kernel's FP32 filter, as rt_api.hip render_async sets it
-  P.flat_recs32 = H.f32.flat_recs.data();
-  P.boxes32 = H.f32.boxes.data();
-  P.flat_filter = RT_F64 && H.flat;
-  if (const char* e = rt_knob("RT_AMD_FLAT_FILTER")) P.flat_filter = P.flat_filter && atoi(e) != 0;
   P.out = out;
   P.surface_root = H.surface_root;
   P.leaf_exit_pct = RT_F64 ? H.leaf_exit_pct64 : H.leaf_exit_pct;
@@ -160,7 +155,6 @@ int render(const HostScene& H, const rt_camera_settings* cs, uint64_t seed, cons
   if (counters) {
     for (int i = 0; i < 3; ++i) counters[i] = s.cnt[i];
     counters[3] = (long long)tile_pixels * P.cam.spp;
-    counters[4] = s.cnt[4];
   }
   if (s.overflow) {
     err = "BVH traversal stack overflow";

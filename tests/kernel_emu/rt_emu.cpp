@@ -38,7 +38,7 @@ namespace emu64 {
 }  // namespace emu64
 
 namespace rt_emu {
-thread_local long long counters[5];
+thread_local long long counters[4];
 }
 
 namespace {
@@ -48,8 +48,7 @@ thread_local std::string g_err;
 extern "C" {
 const char* rt_emu_last_error(void) { return g_err.c_str(); }
 
-// counters (optional, 5 values): BVH nodes visited, primitives tested, segments, samples, undecided
-// filter lanes (rt_trace.h closest_filtered).
+// counters (optional, 4 values): BVH nodes visited, primitives tested, segments, samples.
 // f64 = 1: the binary64 kernel (out: doubles), else the FP32 kernel (out: floats)
 int rt_emu_render(const rt_camera_settings* cs, const rt_scene* sc, uint64_t seed, const rt_exec* ex, void* out,
                   int nthreads, int chunk, long long* counters, int f64) {

@@ -283,23 +283,6 @@ def test_large_primitive_prefix_is_exact(knobs, gpu, monkeypatch, name, precisio
     assert np.array_equal(a, b, equal_nan=True)
 
 
-@pytest.mark.parametrize("name", ["cornell", "box_gallery"])
-def test_flat_fp32_filter_is_the_per_face_binary64_hit(knobs, gpu, monkeypatch, name):
-    """Binary64 flat kernel: the FP32 closest-hit filter with binary64 winner tests (rt_trace.h
-    closest_filtered) renders the image of one binary64 parallelogram test per face (box groups and
-    the filter off) bit for bit on the GPU, at a full-size Cornell frame's rows too."""
-    fn = {"cornell": scenes.cornell_box, "box_gallery": scenes.box_gallery}[name]
-    for kw in (dict(width=96, spp=8), dict(spp=4)):
-        cs, world, seed = fn(**kw)
-        monkeypatch.delenv("RT_AMD_FLAT_FILTER", raising=False)
-        monkeypatch.delenv("RT_AMD_NO_BOX", raising=False)
-        a = R.raytrace(cs, world, seed, precision="f64")
-        monkeypatch.setenv("RT_AMD_FLAT_FILTER", "0")
-        monkeypatch.setenv("RT_AMD_NO_BOX", "1")
-        b = R.raytrace(cs, world, seed, precision="f64")
-        assert np.array_equal(a, b, equal_nan=True), (name, kw)
-
-
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("name", ["cornell", "box_gallery"])
 def test_box_groups_match_oracle(knobs, gpu, oracle_mod, monkeypatch, name, precision):

@@ -225,25 +225,6 @@ def test_box_groups_match_per_face_tests(knobs, oracle_mod, emu_mod, monkeypatch
     np.testing.assert_allclose(a.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=5e-3)
 
 
-@pytest.mark.parametrize("name", ["cornell", "box_gallery", "readme"])
-def test_flat_fp32_filter_is_the_per_face_binary64_hit(knobs, emu_mod, monkeypatch, name):
-    """The binary64 flat kernel's FP32 filter (rt_trace.h closest_filtered: every record tested in
-    FP32 with an error bound, the winner — a box group's face by its own record — in binary64, the
-    undecided lanes in full) renders exactly the image of one binary64 parallelogram test per face
-    (RT_AMD_NO_BOX, filter off): same t, same winner, bit for bit; and it leaves only a few lanes
-    undecided.  README's spheres keep the unfiltered path (DevFlatSet.filt_ok)."""
-    fn = {"cornell": scenes.cornell_box, "box_gallery": scenes.box_gallery, "readme": scenes.readme_scene}[name]
-    cs, world, seed = fn(width=64, spp=8)
-    a, ca = emu_mod.render(cs, world, seed, counters=True)
-    monkeypatch.setenv("RT_AMD_FLAT_FILTER", "0")
-    monkeypatch.setenv("RT_AMD_NO_BOX", "1")
-    b = emu_mod.render(cs, world, seed)
-    assert np.array_equal(a, b, equal_nan=True)
-    assert ca["filter_undecided"] <= 1e-3 * ca["segments"], ca
-    if name == "readme":
-        assert ca["filter_undecided"] == 0
-
-
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("n", [1, 3, 8])
 def test_two_level_instancing_matches_oracle(oracle_mod, emu_mod, n, precision):
