@@ -208,6 +208,7 @@ size_t workspace_bytes(size_t tile_pixels, int acc_words, size_t* off_flag, size
   return oc + 256 * 8;  // up to 8 queue head words (rt_render_kernel.h RT_QUEUES)
 }
 
+
 // ws / ws_cap: a caller-held workspace (a multi-device scene's resident one), or null: the render
 // takes one from the stream-ordered pool (hipMallocAsync / hipFreeAsync)
 template <class R>
@@ -241,6 +242,7 @@ int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_
   P.surface_prefix = (s->variant & RT_VAR_BASE) != RT_VAR_FLAT && s->n_nodes > 0 ? 1 : 0;
   P.n_media = s->n_media;
   for (int k = 0; k < s->n_media; ++k) P.media[k] = A.media[k];
+  P.media_late = media_late(P);
   for (int k = 0; k <= RT_MAX_MEDIA; ++k) P.flat_sets[k] = s->flat_sets[k];
   P.stack_depth = s->stack_depth;
   P.lds_nodes = A.lds_nodes;

@@ -979,6 +979,20 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
   return RT_OK;
 }
 
+// media events in the BVH kernels' shading phase (KernelParams::media_late): every medium's
+// boundary is the surface set or a single leaf; env RT_AMD_MEDIA_LATE=0 keeps them in the
+// traversal loop's query chain (A/B, tests)
+template <class R>
+int media_late(const KernelParamsT<R>& P) {
+  if (P.n_media == 0) return 0;
+  for (int m = 0; m < P.n_media; ++m)
+    if (!P.media[m].alias_surface && !(P.media[m].root < 0 && P.media[m].root != RT_EMPTY_ROOT)) return 0;
+  if (const char* e = rt_knob("RT_AMD_MEDIA_LATE")) return atoi(e) != 0;
+  return 1;
+}
+template int media_late<float>(const KernelParamsT<float>&);
+template int media_late<double>(const KernelParamsT<double>&);
+
 FastDiv rt_host_fastdiv(uint32_t d) {
   FastDiv f{0u, 0, d, 0};
   if (d <= 1) return f;

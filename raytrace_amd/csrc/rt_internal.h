@@ -120,6 +120,11 @@
 // rt_knob returns null and every caller (a Haskell program with a stray variable in its
 // environment included) gets the measured defaults.
 const char* rt_knob(const char* name);
+// BVH kernels: the segment's media events in the shading phase (rt_build.cpp; KernelParams::media_late)
+template <class R>
+struct KernelParamsT;
+template <class R>
+int media_late(const KernelParamsT<R>& P);
 // host choice of variant (rt_build.cpp); knob RT_AMD_VARIANT overrides the base for experiments
 int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, bool inst = false, int leaf_kind = 0);
 
@@ -306,6 +311,9 @@ struct KernelParamsT {
   int surface_root;
   int surface_prefix;         // BVH scenes: flat_sets[0] is the surface set's prefix (rt_trace.h prefix_hits)
   int n_media;
+  // BVH kernels: every medium's boundary is the surface set (alias_surface) or a single leaf, so
+  // the segment's media events run in the shading phase (rt_trace.h media_events_late)
+  int media_late;
   int n_targets;
   R rem_prob;
   DevMediumT<R> media[RT_MAX_MEDIA];

@@ -1740,6 +1740,38 @@ RT_FN int lane_loop_lockstep(const KernelParams& P0, Work& work, const Trav& TW,
   return overflow;
 }
 
+// The segment's media events after its surface query, with the lanes that shade (KernelParams::
+// media_late: every medium's boundary is the surface set or a single leaf, whose records are the
+// same for every lane), instead of a query chain inside the traversal loop run by the few lanes
+// whose query just ended.  Same queries, same draws, same order as the chain (Geometry.hs:306-328):
+// per medium its first boundary hit on (tmin, inf) and, for a ray entering it before the closest
+// hit so far, the second; the images are bit-identical (RT_AMD_MEDIA_LATE=0 runs the chain).
+template <bool kInst>
+RT_FN void media_events_late(const KernelParams& P, cfp prims, const RayCtx& R, TravState& S, uint32_t pix, int sample,
+                             int seg, int best, real t_surf, real& tbest, int& hit_medium) {
+  for (int m = 0; m < P.n_media; ++m) {
+    const DevMedium& M = P.media[m];
+    if (M.alias_surface) {  // the surface hit is the boundary's first hit (DevMedium)
+      if (best >= 0 && !prim_front(P, prims, best, R, t_surf))
+        medium_event(P, m, pix, sample, seg, kTmin, t_surf, tbest, hit_medium);
+      continue;
+    }
+    trav_begin(S, M.root, kTmin);  // a single leaf: parked, tested in place
+    test_leaf_generic<kInst>(P, R, S);
+    if (S.C.prim < 0) continue;
+    const real t1 = S.C.t;
+    if (prim_front(P, prims, S.C.prim, R, t1)) {
+      if (t1 < tbest) {  // entering: the exit hit bounds the segment
+        trav_begin(S, M.root, t1);
+        test_leaf_generic<kInst>(P, R, S);
+        if (S.C.prim >= 0) medium_event(P, m, pix, sample, seg, t1, S.C.t, tbest, hit_medium);
+      }
+    } else {
+      medium_event(P, m, pix, sample, seg, kTmin, t1, tbest, hit_medium);
+    }
+  }
+}
+
 // The persistent lane loop of the BVH kernel, with traversal decoupled from shading inside the
 // wave.  Incoherent secondary rays need very different numbers of traversal rounds; if every
 // lane waited for the wave's slowest traversal before shading, most lanes would idle (measured
@@ -1835,7 +1867,8 @@ RT_FN int lane_loop_bvh(const KernelParams& P0, Work& work, const Trav& TW, cons
             tbest = t_surf = S.C.t;
             best = S.C.prim;
             best_inst = S.C.inst;
-            next_m = 0;
+            // media events in the shading phase (media_events_late): the segment is traced
+            next_m = kMedia && P.media_late ? n_media : 0;
           } else {
             const int m = (q - 1) >> 1;
             next_m = m + 1;
@@ -1886,6 +1919,8 @@ RT_FN int lane_loop_bvh(const KernelParams& P0, Work& work, const Trav& TW, cons
     // ---- shade the segments whose queries are complete
     if (state == ST_SHADE) {
       const KernelParams& P = RT_KARGS(P0);
+      if constexpr (kMedia)
+        if (P.media_late) media_events_late<kInst>(P, prims, R, S, I.pix, I.sample, seg, best, t_surf, tbest, hit_medium);
       f3 L = mk3(RL(0.), RL(0.), RL(0.));
       if (shade<kTex, kMats, kInst>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T, best_inst)) {
         // the path ended: R and T are indeterminate until camera_ray (shade's invariant)

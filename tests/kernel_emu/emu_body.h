@@ -107,6 +107,7 @@ int render(const HostScene& H, const rt_camera_settings* cs, uint64_t seed, cons
   P.surface_prefix = H.flat ? 0 : 1;
   P.n_media = H.n_media;
   for (int k = 0; k < H.n_media; ++k) P.media[k] = A.media[k];
+  P.media_late = media_late(P);
   for (int k = 0; k <= RT_MAX_MEDIA; ++k) P.flat_sets[k] = H.flat_sets[k];
   P.stack_depth = H.max_depth > 1 ? H.max_depth : 1;
   P.n_prims = H.n_prims;

@@ -358,6 +358,19 @@ def test_one_class_leaf_kernels_are_exact(knobs, gpu, monkeypatch, name, precisi
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("name", ["pawn_fog", "demo2"])
+def test_media_events_in_shading_phase_are_exact(knobs, gpu, monkeypatch, name, precision):
+    """The media events in the shading phase (rt_trace.h media_events_late) render the traversal
+    loop's query-chain image bit for bit (RT_AMD_MEDIA_LATE=0)."""
+    fn = {"pawn_fog": scenes.pawn_fog, "demo2": scenes.demo2}[name]
+    cs, world, seed = fn(width=80, spp=8)
+    a = R.raytrace(cs, world, seed, precision=precision)
+    monkeypatch.setenv("RT_AMD_MEDIA_LATE", "0")
+    b = R.raytrace(cs, world, seed, precision=precision)
+    assert np.array_equal(a, b, equal_nan=True)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
 def test_medium_boundary_alias_is_exact(knobs, gpu, monkeypatch, precision):
     cs, world, seed = scenes.pawn_fog(width=96, spp=8)
     a = R.raytrace(cs, world, seed, precision=precision)

@@ -174,6 +174,21 @@ def test_medium_boundary_alias_is_exact(knobs, emu_mod, monkeypatch, variant):
     assert np.array_equal(a, b, equal_nan=True)
 
 
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("name", ["pawn_fog", "pawn_test", "demo2"])
+def test_media_events_in_shading_phase_are_exact(knobs, emu_mod, monkeypatch, name, precision):
+    """BVH kernels whose media boundaries are the surface set or single leaves (pawn+fog: the
+    pawn's interior aliases the surface, the fog is one sphere) run the segment's media events in
+    the shading phase (rt_trace.h media_events_late) instead of the traversal loop's query chain:
+    the same queries, draws and order, so the image is bit-identical (RT_AMD_MEDIA_LATE=0)."""
+    fn = {"pawn_fog": scenes.pawn_fog, "pawn_test": scenes.pawn_test, "demo2": scenes.demo2}[name]
+    cs, world, seed = fn(width=48, spp=4)
+    a = emu_mod.render(cs, world, seed, precision=precision)
+    monkeypatch.setenv("RT_AMD_MEDIA_LATE", "0")
+    b = emu_mod.render(cs, world, seed, precision=precision)
+    assert np.array_equal(a, b, equal_nan=True)
+
+
 @pytest.mark.parametrize("variant", ["1", "2"])
 @pytest.mark.parametrize("name", ["bunny_cornell", "demo1"])
 def test_large_primitive_prefix_is_exact(knobs, emu_mod, monkeypatch, variant, name):
