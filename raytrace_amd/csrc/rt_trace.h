@@ -1364,6 +1364,12 @@ RT_FN void camera_ray(const KernelParams& P, uint32_t pix, int sample, uint32_t 
 // constantMedium's free-flight draw over the segment (lo, hi) (Geometry.hs:312-328); wm is the
 // Philox block of event RT_EV_MEDIA + m / 4 of this segment
 RT_FN void medium_draw(const KernelParams& P, int m, u4 wm, real lo, real hi, real& tbest, int& hit_medium) {
+  // no FMA contraction of lo + hit_dist (the reference's two roundings, Geometry.hs:320-322): the
+  // compiler's choice would otherwise depend on where the draw is inlined, and the media_late and
+  // query-chain kernels must agree bit for bit
+#ifndef RT_HOST_EMU
+#pragma clang fp contract(off)
+#endif
   uint32_t wsel = (m & 3) == 0 ? wm.x : (m & 3) == 1 ? wm.y : (m & 3) == 2 ? wm.z : wm.w;
   real rnd = RL(1.0) - u01(wsel);
   real hit_dist = P.media[m].neg_inv_density * RT_LOG(rnd);
