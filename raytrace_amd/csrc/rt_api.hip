@@ -242,7 +242,6 @@ int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_
   P.surface_prefix = (s->variant & RT_VAR_BASE) != RT_VAR_FLAT && s->n_nodes > 0 ? 1 : 0;
   P.n_media = s->n_media;
   for (int k = 0; k < s->n_media; ++k) P.media[k] = A.media[k];
-  P.media_late = media_late(P);
   for (int k = 0; k <= RT_MAX_MEDIA; ++k) P.flat_sets[k] = s->flat_sets[k];
   P.stack_depth = s->stack_depth;
   P.lds_nodes = A.lds_nodes;
@@ -341,7 +340,8 @@ int upload_common(const std::shared_ptr<const HostScene>& Hp, int device, rt_dev
   s->n_prims = H.n_prims;
   s->max_depth = H.max_depth;
   s->stack_depth = H.max_depth > 1 ? H.max_depth : 1;
-  s->variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex, H.n_instances > 0, H.leaf_kind);
+  s->variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex, H.n_instances > 0, H.leaf_kind,
+                               rt_host_media_late(H));
   s->upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = s;
   return RT_OK;

@@ -872,10 +872,14 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   return RT_OK;
 }
 
-int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, bool inst, int leaf_kind) {
+int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, bool inst, int leaf_kind, bool media_late) {
   int v = flat ? RT_VAR_FLAT : RT_VAR_BVH;
+  // media events in the shading phase; env RT_AMD_MEDIA_LATE=0 keeps them in the traversal loop's
+  // query chain (A/B, tests: the images are bit-identical)
+  if (const char* e = rt_knob("RT_AMD_MEDIA_LATE")) media_late = media_late && atoi(e) != 0;
+  const int late = n_media > 0 && media_late ? RT_VAR_MEDIA_LATE : 0;
   if (inst) return RT_VAR_BVH | RT_VAR_INST | (noise ? RT_VAR_NOISE : 0) | (n_media > 0 ? RT_VAR_MEDIA : 0) |
-                   (mats ? RT_VAR_MATS : 0) | (tex ? RT_VAR_TEX : 0);  // two-level traversal: the decoupled BVH loop
+                   (mats ? RT_VAR_MATS : 0) | (tex ? RT_VAR_TEX : 0) | late;  // two-level traversal: the decoupled BVH loop
   if (const char* e = rt_knob("RT_AMD_VARIANT")) {
     const int f = atoi(e);
     // (the lockstep kernels exist only in experiment builds, RT_LOCKSTEP_KERNELS)
@@ -890,7 +894,7 @@ int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, boo
   if (const char* e = rt_knob("RT_AMD_LEAF_KIND"))
     if (atoi(e) == 0) leaf = 0;
   return v | (noise ? RT_VAR_NOISE : 0) | (n_media > 0 ? RT_VAR_MEDIA : 0) | (mats ? RT_VAR_MATS : 0) |
-         (tex ? RT_VAR_TEX : 0) | leaf;
+         (tex ? RT_VAR_TEX : 0) | leaf | (v == RT_VAR_BVH ? late : 0);
 }
 
 template <class R>
@@ -979,19 +983,14 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
   return RT_OK;
 }
 
-// media events in the BVH kernels' shading phase (KernelParams::media_late): every medium's
-// boundary is the surface set or a single leaf; env RT_AMD_MEDIA_LATE=0 keeps them in the
-// traversal loop's query chain (A/B, tests)
-template <class R>
-int media_late(const KernelParamsT<R>& P) {
-  if (P.n_media == 0) return 0;
-  for (int m = 0; m < P.n_media; ++m)
-    if (!P.media[m].alias_surface && !(P.media[m].root < 0 && P.media[m].root != RT_EMPTY_ROOT)) return 0;
-  if (const char* e = rt_knob("RT_AMD_MEDIA_LATE")) return atoi(e) != 0;
-  return 1;
+bool rt_host_media_late(const HostScene& H) {
+  if (H.n_media == 0) return false;
+  for (int m = 0; m < H.n_media; ++m) {  // (the roots and aliases are the same in both precisions)
+    const DevMediumT<double>& M = H.f64.media[m];
+    if (!M.alias_surface && !(M.root < 0 && M.root != RT_EMPTY_ROOT)) return false;
+  }
+  return true;
 }
-template int media_late<float>(const KernelParamsT<float>&);
-template int media_late<double>(const KernelParamsT<double>&);
 
 FastDiv rt_host_fastdiv(uint32_t d) {
   FastDiv f{0u, 0, d, 0};

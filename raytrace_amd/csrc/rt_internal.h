@@ -114,19 +114,17 @@
 #define RT_VAR_INST 64         // flag: the scene has instances (two-level traversal; RT_VAR_BVH only)
 #define RT_VAR_LEAF_TRI 128    // flag: every BVH leaf below a BVH node is a static triangle (RT_VAR_BVH, no instances)
 #define RT_VAR_LEAF_SPHERE 256 // flag: ... a static sphere (idem; kernels without media only)
+#define RT_VAR_MEDIA_LATE 512  // flag (with RT_VAR_MEDIA, RT_VAR_BVH): the media events in the shading phase
 // Experiment knobs (rt_build.cpp): the library reads its RT_AMD_* tuning variables (variant,
 // chunking, aggregation, prefix, box groups, LDS staging, ...) only when RT_AMD_EXPERIMENTS is set
 // to a nonzero value — A/B sessions and the tests that compare code paths set it.  Otherwise
 // rt_knob returns null and every caller (a Haskell program with a stray variable in its
 // environment included) gets the measured defaults.
 const char* rt_knob(const char* name);
-// BVH kernels: the segment's media events in the shading phase (rt_build.cpp; KernelParams::media_late)
-template <class R>
-struct KernelParamsT;
-template <class R>
-int media_late(const KernelParamsT<R>& P);
-// host choice of variant (rt_build.cpp); knob RT_AMD_VARIANT overrides the base for experiments
-int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, bool inst = false, int leaf_kind = 0);
+// host choice of variant (rt_build.cpp); knob RT_AMD_VARIANT overrides the base for experiments.
+// media_late: every medium's boundary is the surface set or a single leaf (rt_host_media_late)
+int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, bool inst = false, int leaf_kind = 0,
+                    bool media_late = false);
 
 #define RT_KIND_MASK 3
 #define RT_FLAG_MOTION 4
@@ -311,9 +309,6 @@ struct KernelParamsT {
   int surface_root;
   int surface_prefix;         // BVH scenes: flat_sets[0] is the surface set's prefix (rt_trace.h prefix_hits)
   int n_media;
-  // BVH kernels: every medium's boundary is the surface set (alias_surface) or a single leaf, so
-  // the segment's media events run in the shading phase (rt_trace.h media_events_late)
-  int media_late;
   int n_targets;
   R rem_prob;
   DevMediumT<R> media[RT_MAX_MEDIA];
@@ -393,6 +388,10 @@ struct rt_exec;
 int rt_host_build_scene(const rt_scene* sc, HostScene& out, std::string& err);
 int rt_host_image_height(const rt_camera_settings* cs);
 int rt_host_shard_rows(int height, const rt_exec* ex);
+// every medium's boundary is the surface set (alias_surface) or a single leaf, whose records are
+// the same for every lane: the BVH kernels can run the media events in the shading phase
+// (RT_VAR_MEDIA_LATE; rt_trace.h media_events_late)
+bool rt_host_media_late(const HostScene& H);
 // fills camera / targets / tiling / key of P (pointers are left to the caller); R = float, double
 template <class R>
 int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex, KernelParamsT<R>& P,

@@ -28,7 +28,7 @@ namespace RT_NS {
 // and its hardware id — the ramp and the tail of one launch, wave by wave.
 #if defined(RT_WAVE_STAMPS)
 #define RT_STAMP_WAVES 16384
-__device__ unsigned long long rt_stamp_buf[4 * RT_STAMP_WAVES];
+static __device__ unsigned long long rt_stamp_buf[4 * RT_STAMP_WAVES];  // (one per translation unit)
 #endif
 
 namespace {
@@ -333,27 +333,60 @@ struct WaveWork {
 #define RT_WAVES64_FLAT_LITE 5  // 96 VGPRs, no spills (round 4): Cornell binary64 5.442 -> 5.315 ms against 4
 #endif
 #ifndef RT_WAVES64_FLAT
-#define RT_WAVES64_FLAT 2  // readme f64 0.87 -> 0.78 ms at 2 (4: 1.31); the BVH kernels keep 3 (2: demo1 +23 %, pawn+fog +17 %)
+#define RT_WAVES64_FLAT 4  // 100 VGPRs without MachineLICM (round 4: 2, with it 195 VGPRs; readme 0.65 -> 0.46 ms)
 #endif
 #ifndef RT_WAVES64_BVH_LITE
 #define RT_WAVES64_BVH_LITE 4  // 163 ms bunny-Cornell vs 180 at 3 once the BVH nodes were tested in FP32 (profiles/r2/waves64)
 #endif
 #ifndef RT_WAVES64_BVH
-#define RT_WAVES64_BVH 4  // demo1 69.9 ms vs 76.6 at 3 (profiles/r2/waves64)
+#define RT_WAVES64_BVH 4  // demo1 69.9 ms vs 76.6 at 3 (profiles/r2/waves64); textured scenes, instances
+#endif
+#ifndef RT_WAVES64_BVH_MATS
+#define RT_WAVES64_BVH_MATS 5  // constant textures, the full material set (demo1): 57.0 -> 56.4 ms (profiles/r5/licm)
 #endif
 #ifndef RT_WAVES64_BVH_MEDIA
-#define RT_WAVES64_BVH_MEDIA 3  // the media kernels spill more: pawn+fog 641 ms at 3, 883 at 4
+#define RT_WAVES64_BVH_MEDIA 3  // the media chain kernels (pawn+fog 641 ms at 3, 883 at 4), instanced with textures / media
+#endif
+#ifndef RT_WAVES64_BVH_MEDIA_LATE
+#define RT_WAVES64_BVH_MEDIA_LATE 4  // media events in the shading phase (kMedia 2): pawn+fog 508 -> 476 ms
+#endif
+#ifndef RT_WAVES_BVH_MEDIA_LATE
+#define RT_WAVES_BVH_MEDIA_LATE 7  // FP32 pawn+fog 310.7 -> 302 ms against 5 (profiles/r5/licm)
+#endif
+#ifndef RT_WAVES_BVH_MATS
+#define RT_WAVES_BVH_MATS 8  // FP32 BVH, constant textures, the full material set, no media (demo1 39.7 -> 39.25 ms)
 #endif
 #if RT_F64
-#define RT_WAVES_OF(kVar, kTex, kMedia, kMats)                                                     \
+#define RT_WAVES_OF(kVar, kTex, kMedia, kMats, kInst)                                              \
   ((kVar) == RT_VAR_FLAT ? ((kTex) == 0 && !(kMedia) && !(kMats) ? RT_WAVES64_FLAT_LITE : RT_WAVES64_FLAT) \
+                         : (kInst) && ((kTex) != 0 || (kMedia) != 0) ? RT_WAVES64_BVH_MEDIA          \
+                         : (kMedia) == 2 ? RT_WAVES64_BVH_MEDIA_LATE                                \
                          : (kMedia) ? RT_WAVES64_BVH_MEDIA                                          \
-                         : ((kTex) == 0 && !(kMats) ? RT_WAVES64_BVH_LITE : RT_WAVES64_BVH))
+                         : (kTex) == 0 && !(kMats) ? RT_WAVES64_BVH_LITE                            \
+                         : (kTex) == 0 && !(kInst) ? RT_WAVES64_BVH_MATS : RT_WAVES64_BVH)
 #else
-#define RT_WAVES_OF(kVar, kTex, kMedia, kMats)                                                           \
+#define RT_WAVES_OF(kVar, kTex, kMedia, kMats, kInst)                                                    \
   ((kVar) == RT_VAR_FLAT ? ((kTex) == 2 ? RT_WAVES_FLAT_NOISE : (kTex) == 0 ? RT_WAVES_FLAT_TEX0 : RT_WAVES_FLAT) \
+                         : (kMedia) == 2 ? ((kInst) ? RT_WAVES_BVH : RT_WAVES_BVH_MEDIA_LATE)             \
+                         : (kTex) == 0 && !(kMedia) && (kMats) && !(kInst) ? RT_WAVES_BVH_MATS            \
                          : ((kTex) == 0 && !(kMedia) ? RT_WAVES_BVH_LITE : RT_WAVES_BVH))
 #endif
+// Kernels built without MachineLICM (rt_kernel_nl.hip / rt_kernel64_nl.hip, compiled with
+// -mllvm -disable-machine-licm): the pass hoists the loop's binary64 constants (log, sincos and
+// texture polynomial coefficients, ...) out of the persistent lane loop into ~20-90 VGPRs, so the
+// heavier kernels sat at 2-3 waves or spilled (readme binary64 195 VGPRs -> 100: 0.65 -> 0.46 ms;
+// pawn+fog binary64 107 instead of 128 + spills).  The lightest kernels keep it: the Cornell box
+// (flat, constant textures, the diffuse materials) is 1.3 % slower without it and the bunny even
+// (profiles/r5/licm).  Every instantiation lives in exactly one of the two translation units.
+#define RT_NOLICM_OF(kVar, kTex, kMedia, kMats, kInst)                                  \
+  ((kVar) == RT_VAR_FLAT ? (RT_F64 && ((kTex) != 0 || (kMedia) != 0 || (kMats)))       \
+                         : ((kTex) != 0 || (kMedia) != 0 || (kMats) || (kInst)))
+#ifndef RT_TU_NOLICM
+#define RT_TU_NOLICM 0
+#endif
+// kMedia of a variant code (rt_render_kernel's template parameter)
+#define RT_MEDIA_OF(variant) \
+  (((variant) & RT_VAR_MEDIA) == 0 ? 0 : ((variant) & RT_VAR_MEDIA_LATE) && ((variant) & RT_VAR_BASE) == RT_VAR_BVH ? 2 : 1)
 // BVH workgroup size of a kernel class: each workgroup stages its own LDS copy of the top BVH
 // nodes, so the fewer workgroups share a CU the more nodes each copy holds (pawn+fog and demo1
 // gain 6-13 % from staging).  The largest workgroup whose waves split evenly over the
@@ -365,21 +398,23 @@ struct WaveWork {
 #ifndef RT_BLOCK_BVH_OF
 #define RT_BLOCK_BVH_OF(w) (RT_BIG_WG && ((w) == 3 || (w) == 6) ? 768 : RT_BIG_WG && (w) == 4 ? 512 : RT_BLOCK_BVH)
 #endif
-#define RT_BLOCK_OF(kVar, kTex, kMedia, kMats) \
-  ((kVar) == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH_OF(RT_WAVES_OF(kVar, kTex, kMedia, kMats)))
+#define RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst) \
+  ((kVar) == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH_OF(RT_WAVES_OF(kVar, kTex, kMedia, kMats, kInst)))
 // commit-aggregation slots per wave and pixels per slot of a kernel class (rt_internal.h)
 #define RT_AGG_SLOTS_OF(kVar) ((kVar) == RT_VAR_FLAT ? RT_AGG_SLOTS_FLAT : RT_AGG_SLOTS_BVH)
 #define RT_AGG_PIX_OF(kVar) ((kVar) == RT_VAR_FLAT ? RT_AGG_PIX_FLAT : RT_AGG_PIX_BVH)
-template <int kVar, int kTex, bool kMedia, bool kMats, bool kInst, int kLeaf>
-__global__ __launch_bounds__(RT_BLOCK_OF(kVar, kTex, kMedia, kMats))
-__attribute__((amdgpu_waves_per_eu(RT_WAVES_OF(kVar, kTex, kMedia, kMats))))
+// kMedia: 0 none; 1 the media queries chained in the traversal loop; 2 the media events in the
+// shading phase (RT_VAR_MEDIA_LATE; rt_trace.h media_events_late)
+template <int kVar, int kTex, int kMedia, bool kMats, bool kInst, int kLeaf>
+__global__ __launch_bounds__(RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst))
+__attribute__((amdgpu_waves_per_eu(RT_WAVES_OF(kVar, kTex, kMedia, kMats, kInst))))
 void rt_render_kernel(KernelParams P) {
   extern __shared__ int smem[];
 #if defined(RT_WAVE_STAMPS)
   const unsigned long long t_start = wall_clock64();
 #endif
   constexpr int kSlots = RT_AGG_SLOTS_OF(kVar), kPix = RT_AGG_PIX_OF(kVar);
-  constexpr int kBlock = RT_BLOCK_OF(kVar, kTex, kMedia, kMats);
+  constexpr int kBlock = RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst);
   constexpr int kAggBytes = AggGeom<kSlots, kPix>::kWaveBytes;
   const int waves = (int)(gridDim.x * (blockDim.x / 64));
   // wave-uniform (readfirstlane: the compiler cannot tell that threadIdx.x / 64 is), so the work
@@ -416,7 +451,7 @@ void rt_render_kernel(KernelParams P) {
 #endif
   if constexpr (kVar == RT_VAR_FLAT) {
     WaveWork<kSlots, kPix, true> work(P, wave, waves, agg);
-    overflow = lane_loop_lockstep<true, kTex, kMedia, kMats>(P, work, Trav{nullptr, 0, nullptr}, P.prims, acc);
+    overflow = lane_loop_lockstep<true, kTex, kMedia != 0, kMats>(P, work, Trav{nullptr, 0, nullptr}, P.prims, acc);
     work.finish();
     RT_STAMP_END(work)
   } else {
@@ -430,7 +465,7 @@ void rt_render_kernel(KernelParams P) {
     WaveWork<kSlots, kPix, RT_KARGS_WORK_BVH> work(P, wave, waves, agg);
     const Trav W{smem_rest + threadIdx.x, kBlock, lds_nodes};
     if constexpr (kVar == RT_VAR_BVH_LOCKSTEP)
-      overflow = lane_loop_lockstep<false, kTex, kMedia, kMats>(P, work, W, P.prims, acc);
+      overflow = lane_loop_lockstep<false, kTex, kMedia != 0, kMats>(P, work, W, P.prims, acc);
     else
       overflow = lane_loop_bvh<kTex, kMedia, kMats, kInst, kLeaf>(P, work, W, P.prims, acc);
     work.finish();
@@ -439,6 +474,8 @@ void rt_render_kernel(KernelParams P) {
   if (overflow) atomicOr(P.status, 1);
 }
 
+#ifndef RT_KERNEL_ONLY  // (register probes of one instantiation: tools/reg_probe.sh)
+#if !RT_TU_NOLICM  // (the main translation unit)
 // mean over spp (Ray.hs:232) from the fixed-point sums; NaN where a sample was non-finite.  One
 // thread per output word (blockIdx.y = the channel) and the FP32 scale from the host: the kernel
 // needs at most 8 VGPRs, so with two streams it fits beside the next frame's 7-wave FP32 render
@@ -473,14 +510,15 @@ __global__ __launch_bounds__(256) void rt_resolve_kernel(const long long* __rest
   out[w] = bad ? __builtin_nanf("") : (float)((double)accum[3 * (size_t)i + blockIdx.y] * scale);  // scale = 2^-32 / spp
 #endif
 }
+#endif
 
 // the workgroup size of a variant's kernel (RT_BLOCK_OF of its class)
 static int render_block(int variant) {
   const bool flat = (variant & RT_VAR_BASE) == RT_VAR_FLAT;
   const int tex = (variant & RT_VAR_NOISE) ? 2 : (variant & RT_VAR_TEX) ? 1 : 0;
-  const bool media = (variant & RT_VAR_MEDIA) != 0, mats = (variant & RT_VAR_MATS) != 0;
-  (void)mats;
-  return RT_BLOCK_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats);
+  const int media = RT_MEDIA_OF(variant);
+  const bool mats = (variant & RT_VAR_MATS) != 0, inst = (variant & RT_VAR_INST) != 0;
+  return RT_BLOCK_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats, inst);
 }
 static bool acc_in_lds(int variant) {
   return RT_ACC_LDS_OF((variant & RT_VAR_BASE) == RT_VAR_FLAT ? RT_VAR_FLAT : RT_VAR_BVH, (variant & RT_VAR_MEDIA) != 0);
@@ -510,25 +548,42 @@ typedef void (*render_fn)(KernelParams);
 #ifndef RT_LEAF_MEDIA
 #define RT_LEAF_MEDIA 1
 #endif
-template <int kVar, int kTex, bool kMedia, bool kInst, int kLeaf>
+// this translation unit's instantiation, or null when the other one holds it (RT_NOLICM_OF)
+template <int kVar, int kTex, int kMedia, bool kMats, bool kInst, int kLeaf>
+static render_fn kernel_here() {
+  if constexpr ((bool)(RT_NOLICM_OF(kVar, kTex, kMedia, kMats, kInst)) == (bool)RT_TU_NOLICM)
+    return rt_render_kernel<kVar, kTex, kMedia, kMats, kInst, kLeaf>;
+  else
+    return nullptr;
+}
+template <int kVar, int kTex, int kMedia, bool kInst, int kLeaf>
 static render_fn render_kernel_mats(int variant) {
-  return (variant & RT_VAR_MATS) ? rt_render_kernel<kVar, kTex, kMedia, true, kInst, kLeaf>
-                                 : rt_render_kernel<kVar, kTex, kMedia, false, kInst, kLeaf>;
+  return (variant & RT_VAR_MATS) ? kernel_here<kVar, kTex, kMedia, true, kInst, kLeaf>()
+                                 : kernel_here<kVar, kTex, kMedia, false, kInst, kLeaf>();
 }
 template <int kVar, int kTex, bool kInst>
 static render_fn render_kernel_media(int variant) {
   // one-class BVH leaves (RT_VAR_LEAF_*): the decoupled kernel without instances; with media,
   // triangle leaves and constant textures only (pawn+fog)
   if (variant & RT_VAR_MEDIA) {
+    // the decoupled kernel's media events: the traversal loop's query chain, or the shading phase
+    // (RT_VAR_MEDIA_LATE)
+    if constexpr (kVar == RT_VAR_BVH) {
+      if (variant & RT_VAR_MEDIA_LATE) {
+        if constexpr (!kInst && kTex == 0 && RT_LEAF_MEDIA)
+          if (variant & RT_VAR_LEAF_TRI) return render_kernel_mats<kVar, kTex, 2, kInst, 1>(variant);
+        return render_kernel_mats<kVar, kTex, 2, kInst, 0>(variant);
+      }
+    }
     if constexpr (kVar == RT_VAR_BVH && !kInst && kTex == 0 && RT_LEAF_MEDIA)
-      if (variant & RT_VAR_LEAF_TRI) return render_kernel_mats<kVar, kTex, true, kInst, 1>(variant);
-    return render_kernel_mats<kVar, kTex, true, kInst, 0>(variant);
+      if (variant & RT_VAR_LEAF_TRI) return render_kernel_mats<kVar, kTex, 1, kInst, 1>(variant);
+    return render_kernel_mats<kVar, kTex, 1, kInst, 0>(variant);
   }
   if constexpr (kVar == RT_VAR_BVH && !kInst) {
-    if (variant & RT_VAR_LEAF_TRI) return render_kernel_mats<kVar, kTex, false, kInst, 1>(variant);
-    if (variant & RT_VAR_LEAF_SPHERE) return render_kernel_mats<kVar, kTex, false, kInst, 2>(variant);
+    if (variant & RT_VAR_LEAF_TRI) return render_kernel_mats<kVar, kTex, 0, kInst, 1>(variant);
+    if (variant & RT_VAR_LEAF_SPHERE) return render_kernel_mats<kVar, kTex, 0, kInst, 2>(variant);
   }
-  return render_kernel_mats<kVar, kTex, false, kInst, 0>(variant);
+  return render_kernel_mats<kVar, kTex, 0, kInst, 0>(variant);
 }
 template <int kVar, bool kInst>
 static render_fn render_kernel_flags(int variant) {
@@ -537,7 +592,7 @@ static render_fn render_kernel_flags(int variant) {
   return render_kernel_media<kVar, 0, kInst>(variant);
 }
 // two-level instancing (RT_VAR_INST) is compiled into the decoupled BVH kernel only
-static render_fn render_kernel_of(int variant) {
+static render_fn render_kernel_this_tu(int variant) {
   if (variant & RT_VAR_INST) return render_kernel_flags<RT_VAR_BVH, true>(variant);
   switch (variant & RT_VAR_BASE) {
     case RT_VAR_FLAT: return render_kernel_flags<RT_VAR_FLAT, false>(variant);
@@ -547,8 +602,51 @@ static render_fn render_kernel_of(int variant) {
     default: return render_kernel_flags<RT_VAR_BVH, false>(variant);
   }
 }
+// the kernels of the translation unit without MachineLICM (defined there)
+render_fn render_kernel_nolicm(int variant);
+// diagnostic builds: each translation unit's kernels count into that unit's own buffers; the
+// main unit's readers add the other's (a wave's stamps come from one launch: the other is zero)
+template <class T, size_t N>
+static int diag_read(T (&buf)[N], unsigned long long* out, size_t n) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(buf), n * sizeof(T)) != hipSuccess) return -1;
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(buf)) != hipSuccess) return -1;
+  return hipMemset(p, 0, sizeof(buf)) == hipSuccess ? 0 : -1;
+}
+int diag_read_nolicm(int which, unsigned long long* out, size_t n);  // 0: phase counters, 1: stamps
+static int diag_read_this_tu(int which, unsigned long long* out, size_t n) {
+  (void)which, (void)out, (void)n;
+#if defined(RT_PHASE_PROF)
+  if (which == 0) return diag_read(rt_prof_buf, out, n);
+#endif
+#if defined(RT_WAVE_STAMPS)
+  if (which == 1) return diag_read(rt_stamp_buf, out, n);
+#endif
+  return -1;
+}
+#if RT_TU_NOLICM
+int diag_read_nolicm(int which, unsigned long long* out, size_t n) { return diag_read_this_tu(which, out, n); }
+#endif
+static int diag_read_both(int which, unsigned long long* out, size_t n) {
+  if (hipDeviceSynchronize() != hipSuccess || diag_read_this_tu(which, out, n)) return -1;
+  unsigned long long* other = new unsigned long long[n];
+  const int rc = diag_read_nolicm(which, other, n);
+  for (size_t k = 0; k < n && rc == 0; ++k) out[k] += other[k];
+  delete[] other;
+  return rc;
+}
+#if RT_TU_NOLICM
+render_fn render_kernel_nolicm(int variant) { return render_kernel_this_tu(variant); }
+#else
+static render_fn render_kernel_of(int variant) {
+  const render_fn f = render_kernel_this_tu(variant);
+  return f ? f : render_kernel_nolicm(variant);
+}
+#endif
 
+#endif  // RT_KERNEL_ONLY
 }  // namespace RT_NS
+#if !defined(RT_KERNEL_ONLY) && !RT_TU_NOLICM  // (the launchers: in the main translation unit)
 
 int rt_render_resident_blocks(const KernelParamsT<RT_NS::real>*, int device, int stack_depth, int variant,
                               int lds_nodes) {
@@ -571,9 +669,9 @@ int rt_render_resident_blocks(const KernelParamsT<RT_NS::real>*, int device, int
 int rt_render_waves(const KernelParamsT<RT_NS::real>*, int variant) {
   const bool flat = (variant & RT_VAR_BASE) == RT_VAR_FLAT;
   const int tex = (variant & RT_VAR_NOISE) ? 2 : (variant & RT_VAR_TEX) ? 1 : 0;
-  const bool media = (variant & RT_VAR_MEDIA) != 0, mats = (variant & RT_VAR_MATS) != 0;
-  (void)mats;  // the FP32 occupancy table does not depend on the material set
-  return RT_WAVES_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats);
+  const int media = RT_MEDIA_OF(variant);
+  const bool mats = (variant & RT_VAR_MATS) != 0, inst = (variant & RT_VAR_INST) != 0;
+  return RT_WAVES_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats, inst);
 }
 int rt_render_block(const KernelParamsT<RT_NS::real>*, int variant) { return RT_NS::render_block(variant); }
 int rt_render_acc_lds(const KernelParamsT<RT_NS::real>*, int variant) {
@@ -596,10 +694,7 @@ int rt_launch_render(const KernelParamsT<RT_NS::real>& p, int grid_blocks, int v
 int rt_prof_read_kernel(const KernelParamsT<RT_NS::real>*, unsigned long long* out, int n) {
   using namespace RT_NS;
   if (n > PF_N) n = PF_N;
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rt_prof_buf), n * sizeof(unsigned long long)) != hipSuccess) return -1;
-  unsigned long long zero[PF_N] = {};
-  return hipMemcpyToSymbol(HIP_SYMBOL(rt_prof_buf), zero, sizeof(zero)) == hipSuccess ? n : -1;
+  return diag_read_both(0, out, (size_t)n) == 0 ? n : -1;
 }
 #endif
 
@@ -608,12 +703,7 @@ int rt_prof_read_kernel(const KernelParamsT<RT_NS::real>*, unsigned long long* o
 int rt_stamps_read_kernel(const KernelParamsT<RT_NS::real>*, unsigned long long* out, int n_waves) {
   using namespace RT_NS;
   if (n_waves > RT_STAMP_WAVES) n_waves = RT_STAMP_WAVES;
-  const size_t bytes = 4 * sizeof(unsigned long long) * (size_t)n_waves;
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rt_stamp_buf), bytes) != hipSuccess) return -1;
-  void* p = nullptr;
-  if (hipGetSymbolAddress(&p, HIP_SYMBOL(rt_stamp_buf)) != hipSuccess) return -1;
-  return hipMemset(p, 0, sizeof(rt_stamp_buf)) == hipSuccess ? n_waves : -1;
+  return diag_read_both(1, out, 4 * (size_t)n_waves) == 0 ? n_waves : -1;
 }
 #endif
 
@@ -626,3 +716,4 @@ int rt_launch_resolve(const KernelParamsT<RT_NS::real>& p, void* stream) {
                      p.cam.width, p.out_frame_rows, p.n_shards, p.shard, p.row_block);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+#endif  // RT_KERNEL_ONLY

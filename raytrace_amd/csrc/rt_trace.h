@@ -387,7 +387,7 @@ struct RayCtx {
 #else
   f3 idir, oidir;
 #endif
-  real time;
+  uint32_t time_w;  // the ray's time as its Philox word: time = u01(time_w), exact (one VGPR in binary64)
   int self_gid;   // the leaf the ray leaves (skipped: FP32 robustness, rt_trace.h isect_*)
   int self_inst;  // ... and its instance (-1: a world leaf; two-level instancing, RT_VAR_INST)
 };
@@ -398,7 +398,9 @@ RT_FN bool is_self(const RayCtx& R, int gid, int cur_inst) {
   return gid == R.self_gid;
 }
 
-RT_FN f3 motion_shift(const KernelParams& P, int m, real time) {
+RT_FN real u01(uint32_t w);
+RT_FN f3 motion_shift(const KernelParams& P, int m, uint32_t time_w) {
+  const real time = u01(time_w);
   f3 v0 = ldc3(cf(P.motions) + 8 * m), v1 = ldc3(cf(P.motions) + 8 * m + 4);
   return (RL(1.0) - time) * v0 + time * v1;
 }
@@ -616,7 +618,7 @@ RT_FN void test_rec(const KernelParams& P, const PrimRec& r, int pi, const RayCt
   RT_COUNT(1);
   const int kf = RT_R2I(r.a.w);
   f3 o = R.o;
-  if (kf & RT_FLAG_MOTION) o = o - motion_shift(P, RT_R2I(r.e.w), R.time);
+  if (kf & RT_FLAG_MOTION) o = o - motion_shift(P, RT_R2I(r.e.w), R.time_w);
   const bool self = is_self<kInst>(R, RT_R2I(r.b.w), cur_inst);
   real t, q;
   if ((kf & RT_KIND_MASK) == 0)
@@ -775,7 +777,7 @@ RT_FN bool prim_front(const KernelParams& P, cfp prims, int pi, const RayCtx& R,
   int kf = RT_R2I(a.w);
   if ((kf & RT_KIND_MASK) == 0) {
     f3 c = xyz(a);
-    if (kf & RT_FLAG_MOTION) c = c + motion_shift(P, RT_R2I(pr[15]), R.time);
+    if (kf & RT_FLAG_MOTION) c = c + motion_shift(P, RT_R2I(pr[15]), R.time_w);
     f3 p = R.o + t * R.d;
     return dot(R.d, p - c) * (pr[4] < RL(0.0) ? -RL(1.0) : RL(1.0)) <= RL(0.0);
   }
@@ -793,7 +795,7 @@ RT_FN HitInfo surface_info(const KernelParams& P, cfp prims, int pi, const RayCt
   h.gid = RT_R2I(b.w);
   if ((kf & RT_KIND_MASK) == 0) {
     f3 c = xyz(a);
-    if (kf & RT_FLAG_MOTION) c = c + motion_shift(P, RT_R2I(pr[15]), R.time);
+    if (kf & RT_FLAG_MOTION) c = c + motion_shift(P, RT_R2I(pr[15]), R.time_w);
     f3 outward = RT_RCP(b.x) * (h.p - c);
     h.front = dot(R.d, outward) <= RL(0.0);
     h.n = h.front ? outward : -outward;
@@ -816,7 +818,7 @@ RT_FN HitInfo surface_info(const KernelParams& P, cfp prims, int pi, const RayCt
     h.u = h.v = RL(0.0);
     if (!need_uv) return h;
     f3 o = R.o;
-    if (kf & RT_FLAG_MOTION) o = o - motion_shift(P, RT_R2I(pr[15]), R.time);
+    if (kf & RT_FLAG_MOTION) o = o - motion_shift(P, RT_R2I(pr[15]), R.time_w);
     f3 prel = (o + t * R.d) - xyz(b);
     real aa = dot(prel, ldc3(pr + 8)), bb = dot(prel, ldc3(pr + 12));
     cfp uv = cf(P.prim_uv) + 6 * (size_t)pi;
@@ -1014,7 +1016,7 @@ RT_FN Acc acc_words(const AccLds& A) {
 enum : int { PF_FRONT, PF_TRAV, PF_SHADE, PF_ITERS, PF_ROUNDS, PF_TRACING, PF_LIVE, PF_SHADING, PF_FRONT_LANES,
              PF_NODE_STEPS, PF_NODE_LANES, PF_LEAF_STEPS, PF_LEAF_LANES, PF_NODE_CLK, PF_LEAF_CLK, PF_CAM,
              PF_CAM_LANES, PF_N };
-__device__ unsigned long long rt_prof_buf[PF_N];
+static __device__ unsigned long long rt_prof_buf[PF_N];  // (one per translation unit: rt_render_kernel.h)
 #define RT_PROF_DECL unsigned long long prof[PF_N] = {}; unsigned long long pf_t0 = clock64(), pf_t1;
 #define RT_PROF_MARK(k) (pf_t1 = clock64(), prof[k] += pf_t1 - pf_t0, pf_t0 = pf_t1)
 #define RT_PROF_ADD(k, x) (prof[k] += (unsigned long long)(x))
@@ -1344,7 +1346,7 @@ RT_FN void camera_ray(const KernelParams& P, uint32_t pix, int sample, uint32_t 
     px = (int)(pxgy & 0xffffu);
   }
   u4 w0 = philox(pix, (uint32_t)sample, 0u, RT_EV_CAMERA0, P.key0, P.key1);
-  R.time = u01(w0.z);
+  R.time_w = w0.z;
   f3 origin = ld3(P.cam.center);
   if (P.cam.disk_u[0] != RL(0.0) || P.cam.disk_u[1] != RL(0.0) || P.cam.disk_u[2] != RL(0.0) || P.cam.disk_v[0] != RL(0.0) ||
       P.cam.disk_v[1] != RL(0.0) || P.cam.disk_v[2] != RL(0.0)) {
@@ -1666,7 +1668,7 @@ RT_FN int lane_loop_lockstep(const KernelParams& P0, Work& work, const Trav& TW,
 #else
   R.idir = R.oidir = R.o;
 #endif
-  R.time = RL(0.0);
+  R.time_w = 0u;
   R.self_gid = -1;
   R.self_inst = -1;
   RT_PROF_DECL
@@ -1752,29 +1754,45 @@ RT_FN int lane_loop_lockstep(const KernelParams& P0, Work& work, const Trav& TW,
 // whose query just ended.  Same queries, same draws, same order as the chain (Geometry.hs:306-328):
 // per medium its first boundary hit on (tmin, inf) and, for a ray entering it before the closest
 // hit so far, the second; the images are bit-identical (RT_AMD_MEDIA_LATE=0 runs the chain).
+// A kernel has one of the two compiled in (kMedia 2 / 1, rt_render_kernel.h): the chain's state
+// (query index, entry distance, the surface hit kept apart) and its code cost the pawn+fog
+// binary64 kernel ~40 VGPRs over the bunny's, which held it at 3 waves per SIMD.
 template <bool kInst>
-RT_FN void media_events_late(const KernelParams& P, cfp prims, const RayCtx& R, TravState& S, uint32_t pix, int sample,
-                             int seg, int best, real t_surf, real& tbest, int& hit_medium) {
+RT_FN void media_events_late(const KernelParams& P, cfp prims, const RayCtx& R, uint32_t pix, int sample, int seg, int best,
+                             real t_surf, real& tbest, int& hit_medium) {
   for (int m = 0; m < P.n_media; ++m) {
     const DevMedium& M = P.media[m];
+    // the event's interval (lo, hi), if any; one draw site (one inlined copy of Philox and log)
+    bool ev = false;
+    real lo = kTmin, hi = t_surf;
     if (M.alias_surface) {  // the surface hit is the boundary's first hit (DevMedium)
-      if (best >= 0 && !prim_front(P, prims, best, R, t_surf))
-        medium_event(P, m, pix, sample, seg, kTmin, t_surf, tbest, hit_medium);
-      continue;
-    }
-    trav_begin(S, M.root, kTmin);  // a single leaf: parked, tested in place
-    test_leaf_generic<kInst>(P, R, S);
-    if (S.C.prim < 0) continue;
-    const real t1 = S.C.t;
-    if (prim_front(P, prims, S.C.prim, R, t1)) {
-      if (t1 < tbest) {  // entering: the exit hit bounds the segment
-        trav_begin(S, M.root, t1);
-        test_leaf_generic<kInst>(P, R, S);
-        if (S.C.prim >= 0) medium_event(P, m, pix, sample, seg, t1, S.C.t, tbest, hit_medium);
-      }
+      ev = best >= 0 && !prim_front(P, prims, best, R, t_surf);
     } else {
-      medium_event(P, m, pix, sample, seg, kTmin, t1, tbest, hit_medium);
+      // a single leaf: its records from the kernel arguments' root, the same for every lane
+      // (scalar loads, as the surface prefix's), by the generic test
+      const int enc = ~M.root;
+      const int first = enc >> RT_LEAF_SHIFT, end = first + (enc & ((1 << RT_LEAF_SHIFT) - 1)) + 1;
+      Closest C1 = no_hit();
+      for (int k = first; k < end; ++k)
+        test_rec<false, kInst>(P, ld_rec64((const RT_CAS PrimRec64*)prims + k), k, R, kTmin, float_up(kTmin), C1);
+      if (C1.prim >= 0) {
+        const real t1 = C1.t;
+        if (prim_front(P, prims, C1.prim, R, t1)) {
+          if (t1 < tbest) {  // entering: the exit hit bounds the segment
+            Closest C2 = no_hit();
+            for (int k = first; k < end; ++k)
+              test_rec<false, kInst>(P, ld_rec64((const RT_CAS PrimRec64*)prims + k), k, R, t1, float_up(t1), C2);
+            ev = C2.prim >= 0;
+            lo = t1;
+            hi = C2.t;
+          }
+        } else {
+          ev = true;
+          hi = t1;
+        }
+      }
     }
+    if (ev) medium_event(P, m, pix, sample, seg, lo, hi, tbest, hit_medium);
   }
 }
 
@@ -1789,10 +1807,12 @@ RT_FN void media_events_late(const KernelParams& P, cfp prims, const RayCtx& R, 
 // entering it, the second (Geometry.hs:306-328) — each starting inside the traversal loop as
 // soon as the previous one finishes.
 enum : int { ST_NEED_ITEM = 0, ST_NEED_SAMPLE = 1, ST_START_SEG = 2, ST_TRACE = 3, ST_SHADE = 4 };
-template <int kTex, bool kMedia, bool kMats, bool kInst, int kLeaf, class Work, class AccT>
+// kMedia: 0 no media; 1 the media queries chained in the traversal loop; 2 the media events in
+// the shading phase (media_events_late)
+template <int kTex, int kMedia, bool kMats, bool kInst, int kLeaf, class Work, class AccT>
 RT_FN int lane_loop_bvh(const KernelParams& P0, Work& work, const Trav& TW, const real* prims_, AccT& acc) {
   const cfp prims = cf(prims_);
-  const int n_media = kMedia ? P0.n_media : 0;  // media code only in the kMedia instantiations
+  const int n_media = kMedia == 1 ? P0.n_media : 0;  // the chain only in its instantiations
   int overflow = 0;
   ItemCtx I{-1, 0, 0, 0u, 0u};
   int seg = 0;
@@ -1810,12 +1830,15 @@ RT_FN int lane_loop_bvh(const KernelParams& P0, Work& work, const Trav& TW, cons
 #else
   R.idir = R.oidir = R.o;
 #endif
-  R.time = RL(0.0);
+  R.time_w = 0u;
   R.self_gid = -1;
   R.self_inst = -1;
   TravState S;
   trav_begin(S, RT_EMPTY_ROOT, kTmin);
-  // query sequencing within a segment: q = 0 surfaces; q = 1 + 2m / 2 + 2m medium m, 1st / 2nd hit
+  // query sequencing within a segment (the chain, kMedia 1): q = 0 surfaces; q = 1 + 2m / 2 + 2m
+  // medium m, 1st / 2nd hit.  Without the chain the surface query's S.C holds the closest hit
+  // until the shading phase: no loop-carried copies (kMedia 2: the media events take a local one)
+  constexpr bool kChain = kMedia == 1;
   int q = 0, best = -1, hit_medium = -1, best_inst = -1;
   real tbest = kInf, t1 = RL(0.0), t_surf = kInf;
   RT_PROF_DECL
@@ -1869,12 +1892,13 @@ RT_FN int lane_loop_bvh(const KernelParams& P0, Work& work, const Trav& TW, cons
         trav_round<kInst, kLeaf>(P, R, S, TW, overflow RT_PROF_ARG);
         while (trav_done(S)) {
           int next_m = -1;  // medium whose first query starts next
-          if (q == 0) {
-            tbest = t_surf = S.C.t;
-            best = S.C.prim;
-            best_inst = S.C.inst;
-            // media events in the shading phase (media_events_late): the segment is traced
-            next_m = kMedia && P.media_late ? n_media : 0;
+          if (!kChain || q == 0) {
+            if constexpr (kChain) {
+              tbest = t_surf = S.C.t;
+              best = S.C.prim;
+              best_inst = S.C.inst;
+            }
+            next_m = 0;
           } else {
             const int m = (q - 1) >> 1;
             next_m = m + 1;
@@ -1925,8 +1949,14 @@ RT_FN int lane_loop_bvh(const KernelParams& P0, Work& work, const Trav& TW, cons
     // ---- shade the segments whose queries are complete
     if (state == ST_SHADE) {
       const KernelParams& P = RT_KARGS(P0);
-      if constexpr (kMedia)
-        if (P.media_late) media_events_late<kInst>(P, prims, R, S, I.pix, I.sample, seg, best, t_surf, tbest, hit_medium);
+      if constexpr (!kChain) {
+        tbest = S.C.t;
+        best = S.C.prim;
+        best_inst = S.C.inst;
+        hit_medium = -1;
+      }
+      if constexpr (kMedia == 2)  // (tbest is the surface hit's distance until the media events)
+        media_events_late<kInst>(P, prims, R, I.pix, I.sample, seg, best, tbest, tbest, hit_medium);
       f3 L = mk3(RL(0.), RL(0.), RL(0.));
       if (shade<kTex, kMats, kInst>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T, best_inst)) {
         // the path ended: R and T are indeterminate until camera_ray (shade's invariant)

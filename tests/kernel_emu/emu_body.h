@@ -35,7 +35,7 @@ struct Work {
   }
 };
 
-template <int kTex, bool kMedia, bool kMats, class G>
+template <int kTex, int kMedia, bool kMats, class G>
 int run_loop(const RT_NS::KernelParams& P, int variant, G& g, const RT_NS::Trav& W) {
   // the item sums through the device kernels' LDS accumulator (one lane: stride 1)
   unsigned long long words[6] = {0, 0, 0, 0, 0, 0};
@@ -47,9 +47,9 @@ int run_loop(const RT_NS::KernelParams& P, int variant, G& g, const RT_NS::Trav&
       return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, false, 2>(P, g, W, P.prims, acc);
   }
   switch (variant & RT_VAR_BASE) {
-    case RT_VAR_FLAT: return RT_NS::lane_loop_lockstep<true, kTex, kMedia, kMats>(P, g, W, P.prims, acc);
+    case RT_VAR_FLAT: return RT_NS::lane_loop_lockstep<true, kTex, kMedia != 0, kMats>(P, g, W, P.prims, acc);
     case RT_VAR_BVH_LOCKSTEP:
-      return RT_NS::lane_loop_lockstep<false, kTex, kMedia, kMats>(P, g, W, P.prims, acc);
+      return RT_NS::lane_loop_lockstep<false, kTex, kMedia != 0, kMats>(P, g, W, P.prims, acc);
     default: return RT_NS::lane_loop_bvh<kTex, kMedia, kMats, false, 0>(P, g, W, P.prims, acc);
   }
 }
@@ -57,8 +57,11 @@ template <int kTex, class G>
 int run_flags(const RT_NS::KernelParams& P, int variant, G& g, const RT_NS::Trav& W) {
   const int base = variant;
   const bool media = (variant & RT_VAR_MEDIA) != 0, mats = (variant & RT_VAR_MATS) != 0;
-  if (media) return mats ? run_loop<kTex, true, true>(P, base, g, W) : run_loop<kTex, true, false>(P, base, g, W);
-  return mats ? run_loop<kTex, false, true>(P, base, g, W) : run_loop<kTex, false, false>(P, base, g, W);
+  // kMedia as the device kernels (rt_render_kernel.h RT_MEDIA_OF): 2 media events in the shading phase
+  if (media && (variant & RT_VAR_MEDIA_LATE) && (variant & RT_VAR_BASE) == RT_VAR_BVH)
+    return mats ? run_loop<kTex, 2, true>(P, base, g, W) : run_loop<kTex, 2, false>(P, base, g, W);
+  if (media) return mats ? run_loop<kTex, 1, true>(P, base, g, W) : run_loop<kTex, 1, false>(P, base, g, W);
+  return mats ? run_loop<kTex, 0, true>(P, base, g, W) : run_loop<kTex, 0, false>(P, base, g, W);
 }
 template <class G>
 int run_variant(const RT_NS::KernelParams& P, int variant, G& g, const RT_NS::Trav& W) {
@@ -107,11 +110,11 @@ int render(const HostScene& H, const rt_camera_settings* cs, uint64_t seed, cons
   P.surface_prefix = H.flat ? 0 : 1;
   P.n_media = H.n_media;
   for (int k = 0; k < H.n_media; ++k) P.media[k] = A.media[k];
-  P.media_late = media_late(P);
   for (int k = 0; k <= RT_MAX_MEDIA; ++k) P.flat_sets[k] = H.flat_sets[k];
   P.stack_depth = H.max_depth > 1 ? H.max_depth : 1;
   P.n_prims = H.n_prims;
-  const int variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex, H.n_instances > 0, H.leaf_kind);
+  const int variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex, H.n_instances > 0, H.leaf_kind,
+                                      rt_host_media_late(H));
   rt_host_plan_work(P, 4096, (variant & RT_VAR_BASE) == RT_VAR_FLAT);
   P.trav_exit_pct = H.trav_exit_pct;
   if (chunk > 0) {
