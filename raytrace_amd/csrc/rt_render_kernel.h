@@ -378,8 +378,11 @@ struct WaveWork {
 // pawn+fog binary64 107 instead of 128 + spills).  The lightest kernels keep it: the Cornell box
 // (flat, constant textures, the diffuse materials) is 1.3 % slower without it and the bunny even
 // (profiles/r5/licm).  Every instantiation lives in exactly one of the two translation units.
+#ifndef RT_NOLICM_FLAT_LITE
+#define RT_NOLICM_FLAT_LITE 0  // (experiments: the binary64 Cornell kernel without MachineLICM too)
+#endif
 #define RT_NOLICM_OF(kVar, kTex, kMedia, kMats, kInst)                                  \
-  ((kVar) == RT_VAR_FLAT ? (RT_F64 && ((kTex) != 0 || (kMedia) != 0 || (kMats)))       \
+  ((kVar) == RT_VAR_FLAT ? (RT_F64 && (RT_NOLICM_FLAT_LITE || (kTex) != 0 || (kMedia) != 0 || (kMats))) \
                          : ((kTex) != 0 || (kMedia) != 0 || (kMats) || (kInst)))
 #ifndef RT_TU_NOLICM
 #define RT_TU_NOLICM 0

@@ -1660,9 +1660,11 @@ RT_FN int lane_loop_lockstep(const KernelParams& P0, Work& work, const Trav& TW,
   acc_clear(acc);
   bool bad = false;
   bool alive = false;
-  f3 L = mk3(RL(0.), RL(0.), RL(0.)), T = mk3(RL(1.), RL(1.), RL(1.));
+  // T: the path throughput.  No radiance register across iterations (as lane_loop_bvh): only the
+  // event that ends a path emits, so a sample's radiance is that one term, summed at once.
+  f3 T = mk3(RL(1.), RL(1.), RL(1.));
   RayCtx R;
-  R.o = R.d = L;
+  R.o = R.d = mk3(RL(0.), RL(0.), RL(0.));
 #if RT_NODE_F32
   R.idir = R.off0 = R.off1 = f3n{0.f, 0.f, 0.f};
 #else
@@ -1692,7 +1694,6 @@ RT_FN int lane_loop_lockstep(const KernelParams& P0, Work& work, const Trav& TW,
     RT_PROF_ADD(PF_CAM_LANES, RT_BALLOT_COUNT(!alive));
     if (!alive) {
       camera_ray(P, I.pix, I.sample, I.pxgy, R);
-      L = mk3(RL(0.), RL(0.), RL(0.));
       T = mk3(RL(1.), RL(1.), RL(1.));
       seg = 0;
       alive = true;
@@ -1735,6 +1736,7 @@ RT_FN int lane_loop_lockstep(const KernelParams& P0, Work& work, const Trav& TW,
       medium_event(P, m, I.pix, I.sample, seg, lo, hi, tbest, hit_medium);
     }
     RT_PROF_MARK(PF_TRAV);
+    f3 L = mk3(RL(0.), RL(0.), RL(0.));
     if (shade<kTex, kMats>(P, prims, I.pix, I.sample, seg, tbest, best, hit_medium, R, L, T)) {
       // the path ended: R and T are indeterminate until camera_ray (shade's invariant)
       RT_HOOK_SAMPLE(I.pix, I.sample, L);
