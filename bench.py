@@ -510,7 +510,10 @@ def main():
             dist.all_gather_object(allr, mine)
             km = [r["kernel_ms"] for r in allr]
             ranks = {"per_rank": allr, "kernel_ms_min": min(km), "kernel_ms_max": max(km),
-                     "slowest_rank": max(allr, key=lambda r: r["ms_per_step_local"])["rank"],
+                     # the rank whose wall time sets the line's max-over-ranks time, and the one whose
+                     # kernels took longest (they differ when the exchange, not the render, is slow)
+                     "slowest_rank_wall": max(allr, key=lambda r: r["ms_per_step_local"])["rank"],
+                     "slowest_rank_kernel": max(allr, key=lambda r: r["kernel_ms"])["rank"],
                      "note": "kernel_ms: the rank's render device time per frame (HIP events); gather_after_render_ms: "
                              "a frame's render end -> its RCCL all_gather done (probe stream, RCCL only); "
                              "ms_per_step_local: the rank's own timed region / frames before the max over ranks"}
