@@ -210,14 +210,21 @@ size_t workspace_bytes(size_t tile_pixels, int acc_words, size_t* off_flag, size
 
 
 // ws / ws_cap: a caller-held workspace (a multi-device scene's resident one), or null: the render
-// takes one from the stream-ordered pool (hipMallocAsync / hipFreeAsync)
+// takes one from the stream-ordered pool (hipMallocAsync / hipFreeAsync).  lone: a synchronous
+// call's launch (rt_render, rt_multi_render), whose time includes the end of its queue: the flat
+// kernels take 64-id pools there, so no wave holds a second round of items when the queue drains
+// (one binary64 Cornell launch 5.385 -> 5.164 ms; with frames overlapped on two streams, as
+// rt_render_async callers run them, 128 is as fast and the README scene 2 % faster:
+// profiles/r5/pool).  Env RT_AMD_POOL_SHIFT overrides (experiments).
 template <class R>
 int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex, R* d_out,
-                 void* hip_stream, char* ws_given = nullptr, size_t ws_cap = 0, int frame_rows = 0) {
+                 void* hip_stream, char* ws_given = nullptr, size_t ws_cap = 0, int frame_rows = 0, bool lone = false) {
   if (int rc = ensure_precision<R>(s)) return rc;
   const DevArrays<R>& A = s->arrays<R>();
   KernelParamsT<R> P;
   std::memset(&P, 0, sizeof P);
+  if (lone && (s->variant & RT_VAR_BASE) == RT_VAR_FLAT) P.pool_shift = 6;
+  if (const char* e = rt_knob("RT_AMD_POOL_SHIFT")) P.pool_shift = std::max(6, std::min(10, atoi(e)));
   std::string err;
   int rc = rt_host_make_params(cs, seed, ex, P, err);
   if (rc) return fail(rc, "%s", err.c_str());
@@ -493,8 +500,8 @@ int render_one(rt_multi_scene* M, const rt_camera_settings* cs, uint64_t seed, c
   if (int r = grow((void**)&q.ws, &q.ws_cap, wsb, &allocs)) return r;
   HIP_TRY(hipMemsetAsync(s->status, 0, 4 * sizeof(int), q.st));
   HIP_TRY(hipEventRecord(q.e0, q.st));
-  const int r = f32 ? render_async<float>(s, cs, seed, &ex, (float*)q.d_tile, q.st, q.ws, q.ws_cap, 0)
-                    : render_async<double>(s, cs, seed, &ex, (double*)q.d_tile, q.st, q.ws, q.ws_cap, 0);
+  const int r = f32 ? render_async<float>(s, cs, seed, &ex, (float*)q.d_tile, q.st, q.ws, q.ws_cap, 0, true)
+                    : render_async<double>(s, cs, seed, &ex, (double*)q.d_tile, q.st, q.ws, q.ws_cap, 0, true);
   if (r) return r;
   HIP_TRY(hipEventRecord(q.e1, q.st));
   const void* src = q.d_tile;
@@ -619,8 +626,8 @@ int multi_render(rt_multi_scene* M, const rt_camera_settings* cs, uint64_t seed,
           void* dst = direct ? M->d_gather : q.d_tile;
           const int frame_rows = direct ? h : 0;
           HIP_TRY(hipEventRecord(q.e0, q.st));
-          const int r = f32 ? render_async<float>(s, cs, seed, &p.ex, (float*)dst, q.st, q.ws, q.ws_cap, frame_rows)
-                            : render_async<double>(s, cs, seed, &p.ex, (double*)dst, q.st, q.ws, q.ws_cap, frame_rows);
+          const int r = f32 ? render_async<float>(s, cs, seed, &p.ex, (float*)dst, q.st, q.ws, q.ws_cap, frame_rows, true)
+                            : render_async<double>(s, cs, seed, &p.ex, (double*)dst, q.st, q.ws, q.ws_cap, frame_rows, true);
           if (r) return r;
           HIP_TRY(hipEventRecord(q.e1, q.st));
           if (n > 1 && !direct) {

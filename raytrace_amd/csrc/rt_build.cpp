@@ -1006,6 +1006,7 @@ template <class R>
 void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_sizes) {
   P.div_width = rt_host_fastdiv((uint32_t)P.cam.width);
   P.div_block = rt_host_fastdiv((uint32_t)P.row_block);
+  if (P.pool_shift < 6) P.pool_shift = __builtin_ctz(RT_POOL);  // (the caller may set 6: 64-id pools)
   P.trav_exit_pct = 50;  // the caller sets the scene's policy (HostScene::trav_exit_pct) afterwards
   // Items = (tile pixel, chunk of consecutive samples), claimed in pixel order.  Small chunks
   // keep the 64 lanes of a wave on neighbouring pixels (coherent rays) and make the queue tail
@@ -1070,7 +1071,8 @@ void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_s
   // commit aggregation: a phase qualifies when a pool of RT_POOL consecutive ids spans at most a
   // slot's pixels (rt_render_kernel.h WaveWork); env RT_AMD_AGG=0 turns it off (A/B, same LDS)
   const int slot_pix = two_sizes ? RT_AGG_PIX_FLAT : RT_AGG_PIX_BVH;
-  auto spans = [&](int n) { return n > 0 && (RT_POOL - 1 + n - 1) / n + 1 <= slot_pix; };
+  const int pool = 1 << P.pool_shift;
+  auto spans = [&](int n) { return n > 0 && (pool - 1 + n - 1) / n + 1 <= slot_pix; };
   bool agg = tile_pixels < (1ll << 24);  // the item's aggregation code shares its tile-pixel word
   if (const char* env = rt_knob("RT_AMD_AGG")) agg = agg && std::atoi(env) != 0;
   P.agg_big = agg && spans(n_big);

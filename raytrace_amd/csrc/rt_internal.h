@@ -47,7 +47,7 @@
 // Work-item claims: a wave takes RT_POOL consecutive ids per queue atomic (rt_render_kernel.h
 // WaveWork).  64 -> 128: Cornell 4.13 -> 4.04 ms (at 32 the head word saturates: 7.2 ms)
 #ifndef RT_POOL
-#define RT_POOL 128
+#define RT_POOL 128  // (a power of two >= 64; KernelParams::pool_shift)
 #endif
 // Commit aggregation (rt_render_kernel.h WaveWork): per wave, RT_AGG_SLOTS_* LDS slots of
 // RT_AGG_PIX_* pixels' fixed-point words; a pool of RT_POOL ids is aggregated when it lies in one
@@ -301,6 +301,10 @@ struct KernelParamsT {
   // wave's LDS slots when agg_big / agg_small (its chunks per pixel >= RT_AGG_MIN_N of the kernel
   // class); 0: every item adds to `accum` directly
   int agg_big, agg_small;
+  // ids per work-queue pool, 1 << pool_shift (rt_render_kernel.h WaveWork): RT_POOL for renders
+  // whose frames overlap (rt_render_async), 64 for the flat kernels' synchronous calls (rt_api.hip
+  // render_async `lone`), whose one launch ends on the pools still held when the queue drains
+  int pool_shift;
   int stack_depth;            // LDS stack entries per lane (>= the scene's BVH depth)
   int lds_nodes;              // BVH nodes [0, lds_nodes) are read from the workgroup's LDS copy
   int trav_exit_pct;          // BVH kernel: leave traversal when <= this % of live lanes trace

@@ -98,6 +98,7 @@ struct WaveWork {
   // single word saturates at ~88 returning atomics per microsecond, MI355X_MICROARCH.md
   // "dequeue").  Lanes that need work take ids in lane order; ids are never dropped (a pool is
   // contiguous and increasing, so once a lane draws an id >= n_items every later id is too).
+  int pool;    // ids per pool: 1 << kp().pool_shift (the host's choice per launch, RT_POOL by default)
   int pool_base;
   int pool_left;
   int offset;  // ids [0, offset) are the waves' initial pools, handed out without atomics
@@ -115,13 +116,14 @@ struct WaveWork {
   __device__ __forceinline__ const KernelParams& kp() const { return RT_KARGS_IF(kReread, P); }
 
   __device__ __forceinline__ WaveWork(const KernelParams& P_, int wave, int waves, unsigned long long* slots_)
-      : P(P_), pool_base(wave * RT_POOL), pool_left(RT_POOL), offset(waves * RT_POOL), queue(wave & (RT_QUEUES - 1)),
+      : P(P_), pool(1 << P_.pool_shift), pool_base(wave * pool), pool_left(pool), offset(waves * pool),
+        queue(wave & (RT_QUEUES - 1)),
         spent(0), pool_slot(-1), slots(slots_),
         hdr(reinterpret_cast<int*>(slots_ + kSlots * AggGeom<kSlots, kPix>::kWords)),
         free_mask(kSlots > 0 ? (1u << kSlots) - 1u : 0u) {
-    // every wave starts with a static pool (its wave index x RT_POOL): at launch all resident
+    // every wave starts with a static pool (its wave index x pool): at launch all resident
     // waves would otherwise queue up on the counter at once (~80 us at ~88 returning atomics per us)
-    pool_slot = open_pool(pool_base, min(RT_POOL, P.n_items - pool_base));
+    pool_slot = open_pool(pool_base, min(pool, P.n_items - pool_base));
   }
 
   // a slot for the pool of ids [b0, b0 + cnt) (wave-uniform), or -1: commit its items directly.
@@ -175,7 +177,7 @@ struct WaveWork {
     const int leader = __ffsll((unsigned long long)m) - 1;
     const int dyn = n_items - offset;
 #if RT_QUEUE_INTERLEAVE
-    const int n_pools = dyn > 0 ? (dyn + RT_POOL - 1) / RT_POOL : 0;
+    const int n_pools = dyn > 0 ? (dyn + pool - 1) / pool : 0;
 #else
     const int len = dyn > 0 ? (dyn + RT_QUEUES - 1) / RT_QUEUES : 0;
 #endif
@@ -193,7 +195,7 @@ struct WaveWork {
       const int qs = offset + queue * len;
       const int qlen = min(len, n_items - qs);  // <= 0 for an empty last queue
       int base = 0;
-      if (lane == leader) base = atomicAdd(kp().counter + 64 * queue, RT_POOL);
+      if (lane == leader) base = atomicAdd(kp().counter + 64 * queue, pool);
       base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
       if (base >= qlen) {  // spent: ids are only ever handed out below qlen
 #endif
@@ -205,9 +207,9 @@ struct WaveWork {
         continue;
       }
 #if RT_QUEUE_INTERLEAVE
-      const int base = (pk * RT_QUEUES + queue) * RT_POOL;
+      const int base = (pk * RT_QUEUES + queue) * pool;
 #endif
-      const int avail = min(RT_POOL, qlen - base);
+      const int avail = min(pool, qlen - base);
       const int take = min(rest, avail);
       pool_slot = open_pool(qs + base, avail);
       if (rank >= first && rank < first + take) {
@@ -381,9 +383,12 @@ struct WaveWork {
 #ifndef RT_NOLICM_FLAT_LITE
 #define RT_NOLICM_FLAT_LITE 0  // (experiments: the binary64 Cornell kernel without MachineLICM too)
 #endif
+#ifndef RT_NOLICM_BVH_LITE
+#define RT_NOLICM_BVH_LITE 0  // (experiments: the bunny class without MachineLICM too)
+#endif
 #define RT_NOLICM_OF(kVar, kTex, kMedia, kMats, kInst)                                  \
   ((kVar) == RT_VAR_FLAT ? (RT_F64 && (RT_NOLICM_FLAT_LITE || (kTex) != 0 || (kMedia) != 0 || (kMats))) \
-                         : ((kTex) != 0 || (kMedia) != 0 || (kMats) || (kInst)))
+                         : (RT_NOLICM_BVH_LITE || (kTex) != 0 || (kMedia) != 0 || (kMats) || (kInst)))
 #ifndef RT_TU_NOLICM
 #define RT_TU_NOLICM 0
 #endif
