@@ -348,7 +348,7 @@ int upload_common(const std::shared_ptr<const HostScene>& Hp, int device, rt_dev
   s->max_depth = H.max_depth;
   s->stack_depth = H.max_depth > 1 ? H.max_depth : 1;
   s->variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex, H.n_instances > 0, H.leaf_kind,
-                               rt_host_media_late(H));
+                               rt_host_media_late(H), s->stack_depth);
   s->upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = s;
   return RT_OK;

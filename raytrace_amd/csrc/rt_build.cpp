@@ -872,14 +872,18 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
   return RT_OK;
 }
 
-int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, bool inst, int leaf_kind, bool media_late) {
+int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, bool inst, int leaf_kind, bool media_late,
+                    int stack_depth) {
   int v = flat ? RT_VAR_FLAT : RT_VAR_BVH;
+  // the BVH kernels' 1024-lane classes (rt_render_kernel.h RT_BLOCK_BVH_OF) hold RT_WIDE_STACK_ROWS
+  // stack rows per lane; a deeper BVH takes the 512-lane twin of its class
+  const int narrow = !flat && stack_depth + 1 > RT_WIDE_STACK_ROWS ? RT_VAR_NARROW : 0;
   // media events in the shading phase; env RT_AMD_MEDIA_LATE=0 keeps them in the traversal loop's
   // query chain (A/B, tests: the images are bit-identical)
   if (const char* e = rt_knob("RT_AMD_MEDIA_LATE")) media_late = media_late && atoi(e) != 0;
   const int late = n_media > 0 && media_late ? RT_VAR_MEDIA_LATE : 0;
   if (inst) return RT_VAR_BVH | RT_VAR_INST | (noise ? RT_VAR_NOISE : 0) | (n_media > 0 ? RT_VAR_MEDIA : 0) |
-                   (mats ? RT_VAR_MATS : 0) | (tex ? RT_VAR_TEX : 0) | late;  // two-level traversal: the decoupled BVH loop
+                   (mats ? RT_VAR_MATS : 0) | (tex ? RT_VAR_TEX : 0) | late | narrow;  // two-level traversal: the decoupled BVH loop
   if (const char* e = rt_knob("RT_AMD_VARIANT")) {
     const int f = atoi(e);
     // (the lockstep kernels exist only in experiment builds, RT_LOCKSTEP_KERNELS)
@@ -894,7 +898,7 @@ int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, boo
   if (const char* e = rt_knob("RT_AMD_LEAF_KIND"))
     if (atoi(e) == 0) leaf = 0;
   return v | (noise ? RT_VAR_NOISE : 0) | (n_media > 0 ? RT_VAR_MEDIA : 0) | (mats ? RT_VAR_MATS : 0) |
-         (tex ? RT_VAR_TEX : 0) | leaf | (v == RT_VAR_BVH ? late : 0);
+         (tex ? RT_VAR_TEX : 0) | leaf | (v == RT_VAR_BVH ? late : 0) | narrow;
 }
 
 template <class R>

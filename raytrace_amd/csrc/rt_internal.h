@@ -115,6 +115,10 @@
 #define RT_VAR_LEAF_TRI 128    // flag: every BVH leaf below a BVH node is a static triangle (RT_VAR_BVH, no instances)
 #define RT_VAR_LEAF_SPHERE 256 // flag: ... a static sphere (idem; kernels without media only)
 #define RT_VAR_MEDIA_LATE 512  // flag (with RT_VAR_MEDIA, RT_VAR_BVH): the media events in the shading phase
+#define RT_VAR_NARROW 1024     // flag: a 1024-lane kernel class launches its 512-lane twin (a deep BVH's stacks)
+// The deepest stack (rows) one 1024-lane workgroup holds beside its lanes' item sums and slots
+// (binary64: 48 + 16 B per lane; the FP32 classes take the same rule): deeper BVHs run RT_VAR_NARROW
+#define RT_WIDE_STACK_ROWS 23
 // Experiment knobs (rt_build.cpp): the library reads its RT_AMD_* tuning variables (variant,
 // chunking, aggregation, prefix, box groups, LDS staging, ...) only when RT_AMD_EXPERIMENTS is set
 // to a nonzero value — A/B sessions and the tests that compare code paths set it.  Otherwise
@@ -124,7 +128,7 @@ const char* rt_knob(const char* name);
 // host choice of variant (rt_build.cpp); knob RT_AMD_VARIANT overrides the base for experiments.
 // media_late: every medium's boundary is the surface set or a single leaf (rt_host_media_late)
 int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, bool inst = false, int leaf_kind = 0,
-                    bool media_late = false);
+                    bool media_late = false, int stack_depth = 1);
 
 #define RT_KIND_MASK 3
 #define RT_FLAG_MOTION 4

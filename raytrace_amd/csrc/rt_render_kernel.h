@@ -399,12 +399,17 @@ struct WaveWork {
 // nodes, so the fewer workgroups share a CU the more nodes each copy holds (pawn+fog and demo1
 // gain 6-13 % from staging).  The largest workgroup whose waves split evenly over the
 // CU's 4 SIMDs at the kernel's occupancy W (waves per SIMD): W = 3 -> 768 threads (one per CU),
-// 4 -> 512 (two), 6 -> 768 (two); W = 5 keeps 256 (five).  RT_BIG_WG=0: 256 everywhere.
+// 4 -> 1024 (one), 6 -> 768 (two), 8 -> 1024 (two); W = 5 / 7 keep 256.  Round 5 (profiles/r5/
+// bigwg): W = 4 at 1024 instead of 512 stages all of pawn+fog's surface nodes (binary64 476.5 ->
+// 428.1 ms; bunny even); W = 8 at 1024 instead of 256, FP32 demo1 39.35 -> 37.7 ms; 640 / 896
+// threads at W = 5 / 7 do not split evenly (10 / 14 waves per workgroup over 4 SIMDs): demo1
+// binary64 +36 %, pawn+fog FP32 +22 %, one workgroup per CU fits.  RT_BIG_WG=0: 256 everywhere.
 #ifndef RT_BIG_WG
 #define RT_BIG_WG 1
 #endif
 #ifndef RT_BLOCK_BVH_OF
-#define RT_BLOCK_BVH_OF(w) (RT_BIG_WG && ((w) == 3 || (w) == 6) ? 768 : RT_BIG_WG && (w) == 4 ? 512 : RT_BLOCK_BVH)
+#define RT_BLOCK_BVH_OF(w) \
+  (RT_BIG_WG && ((w) == 3 || (w) == 6) ? 768 : RT_BIG_WG && ((w) == 4 || (w) == 8) ? 1024 : RT_BLOCK_BVH)
 #endif
 #define RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst) \
   ((kVar) == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH_OF(RT_WAVES_OF(kVar, kTex, kMedia, kMats, kInst)))
@@ -413,8 +418,12 @@ struct WaveWork {
 #define RT_AGG_PIX_OF(kVar) ((kVar) == RT_VAR_FLAT ? RT_AGG_PIX_FLAT : RT_AGG_PIX_BVH)
 // kMedia: 0 none; 1 the media queries chained in the traversal loop; 2 the media events in the
 // shading phase (RT_VAR_MEDIA_LATE; rt_trace.h media_events_late)
-template <int kVar, int kTex, int kMedia, bool kMats, bool kInst, int kLeaf>
-__global__ __launch_bounds__(RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst))
+// kNarrow: the 1024-lane class at 512 lanes, for a scene whose stacks do not fit one 1024-lane
+// workgroup's LDS (RT_VAR_NARROW)
+#define RT_BLOCK_N(kVar, kTex, kMedia, kMats, kInst, kNarrow) \
+  ((kNarrow) && RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst) == 1024 ? 512 : RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst))
+template <int kVar, int kTex, int kMedia, bool kMats, bool kInst, int kLeaf, bool kNarrow = false>
+__global__ __launch_bounds__(RT_BLOCK_N(kVar, kTex, kMedia, kMats, kInst, kNarrow))
 __attribute__((amdgpu_waves_per_eu(RT_WAVES_OF(kVar, kTex, kMedia, kMats, kInst))))
 void rt_render_kernel(KernelParams P) {
   extern __shared__ int smem[];
@@ -422,7 +431,8 @@ void rt_render_kernel(KernelParams P) {
   const unsigned long long t_start = wall_clock64();
 #endif
   constexpr int kSlots = RT_AGG_SLOTS_OF(kVar), kPix = RT_AGG_PIX_OF(kVar);
-  constexpr int kBlock = RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst);
+  // (the launch bound; a deep BVH's render may launch fewer lanes: host render_block)
+  constexpr int block = RT_BLOCK_N(kVar, kTex, kMedia, kMats, kInst, kNarrow);
   constexpr int kAggBytes = AggGeom<kSlots, kPix>::kWaveBytes;
   const int waves = (int)(gridDim.x * (blockDim.x / 64));
   // wave-uniform (readfirstlane: the compiler cannot tell that threadIdx.x / 64 is), so the work
@@ -431,7 +441,7 @@ void rt_render_kernel(KernelParams P) {
   const int wave = (int)blockIdx.x * (int)(blockDim.x / 64) + wave_in_block;
   int overflow;
   // LDS: the lanes' item sums [RT_ACC_WORDS][block] (rt_trace.h AccLds; BVH kernels), the waves'
-  // commit-aggregation slots (kAggBytes each), then (BVH kernels) [stack_depth + 1][kBlock]
+  // commit-aggregation slots (kAggBytes each), then (BVH kernels) [stack_depth + 1][block]
   // stack words (the last row a spare write target) and the top P.lds_nodes BVH nodes (64 B each)
   using AccT = typename std::conditional<RT_ACC_LDS_OF(kVar, kMedia), AccLds, Acc>::type;
   AccT acc;
@@ -463,15 +473,15 @@ void rt_render_kernel(KernelParams P) {
     work.finish();
     RT_STAMP_END(work)
   } else {
-    v4f* lds_nodes = reinterpret_cast<v4f*>(smem_rest + (P.stack_depth + 1) * kBlock);
+    v4f* lds_nodes = reinterpret_cast<v4f*>(smem_rest + (P.stack_depth + 1) * block);
     const float4* src = reinterpret_cast<const float4*>(P.nodes);
-    for (int i = threadIdx.x; i < 4 * P.lds_nodes; i += kBlock) {
+    for (int i = threadIdx.x; i < 4 * P.lds_nodes; i += block) {
       const float4 q = src[i];
       lds_nodes[i] = v4f{q.x, q.y, q.z, q.w};
     }
     __syncthreads();
     WaveWork<kSlots, kPix, RT_KARGS_WORK_BVH> work(P, wave, waves, agg);
-    const Trav W{smem_rest + threadIdx.x, kBlock, lds_nodes};
+    const Trav W{smem_rest + threadIdx.x, block, lds_nodes};
     if constexpr (kVar == RT_VAR_BVH_LOCKSTEP)
       overflow = lane_loop_lockstep<false, kTex, kMedia != 0, kMats>(P, work, W, P.prims, acc);
     else
@@ -520,13 +530,15 @@ __global__ __launch_bounds__(256) void rt_resolve_kernel(const long long* __rest
 }
 #endif
 
-// the workgroup size of a variant's kernel (RT_BLOCK_OF of its class)
+// the workgroup of a variant's kernel (RT_BLOCK_OF of its class; RT_VAR_NARROW: half the
+// 1024-lane workgroup, rt_build.cpp rt_host_variant)
 static int render_block(int variant) {
   const bool flat = (variant & RT_VAR_BASE) == RT_VAR_FLAT;
   const int tex = (variant & RT_VAR_NOISE) ? 2 : (variant & RT_VAR_TEX) ? 1 : 0;
   const int media = RT_MEDIA_OF(variant);
   const bool mats = (variant & RT_VAR_MATS) != 0, inst = (variant & RT_VAR_INST) != 0;
-  return RT_BLOCK_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats, inst);
+  const int b = RT_BLOCK_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats, inst);
+  return b == 1024 && (variant & RT_VAR_NARROW) ? 512 : b;
 }
 static bool acc_in_lds(int variant) {
   return RT_ACC_LDS_OF((variant & RT_VAR_BASE) == RT_VAR_FLAT ? RT_VAR_FLAT : RT_VAR_BVH, (variant & RT_VAR_MEDIA) != 0);
@@ -558,16 +570,20 @@ typedef void (*render_fn)(KernelParams);
 #endif
 // this translation unit's instantiation, or null when the other one holds it (RT_NOLICM_OF)
 template <int kVar, int kTex, int kMedia, bool kMats, bool kInst, int kLeaf>
-static render_fn kernel_here() {
-  if constexpr ((bool)(RT_NOLICM_OF(kVar, kTex, kMedia, kMats, kInst)) == (bool)RT_TU_NOLICM)
-    return rt_render_kernel<kVar, kTex, kMedia, kMats, kInst, kLeaf>;
-  else
+static render_fn kernel_here(int variant) {
+  if constexpr ((bool)(RT_NOLICM_OF(kVar, kTex, kMedia, kMats, kInst)) == (bool)RT_TU_NOLICM) {
+    if constexpr (RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst) == 1024)  // (the narrow twin)
+      if (variant & RT_VAR_NARROW) return rt_render_kernel<kVar, kTex, kMedia, kMats, kInst, kLeaf, true>;
+    return rt_render_kernel<kVar, kTex, kMedia, kMats, kInst, kLeaf, false>;
+  } else {
+    (void)variant;
     return nullptr;
+  }
 }
 template <int kVar, int kTex, int kMedia, bool kInst, int kLeaf>
 static render_fn render_kernel_mats(int variant) {
-  return (variant & RT_VAR_MATS) ? kernel_here<kVar, kTex, kMedia, true, kInst, kLeaf>()
-                                 : kernel_here<kVar, kTex, kMedia, false, kInst, kLeaf>();
+  return (variant & RT_VAR_MATS) ? kernel_here<kVar, kTex, kMedia, true, kInst, kLeaf>(variant)
+                                 : kernel_here<kVar, kTex, kMedia, false, kInst, kLeaf>(variant);
 }
 template <int kVar, int kTex, bool kInst>
 static render_fn render_kernel_media(int variant) {
@@ -664,7 +680,8 @@ int rt_render_resident_blocks(const KernelParamsT<RT_NS::real>*, int device, int
   if (lds > 65536 && hipFuncSetAttribute((const void*)render_kernel_of(variant),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -1;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_kernel_of(variant), render_block(variant), lds);
+  hipError_t e =
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_kernel_of(variant), render_block(variant), lds);
   if (e != hipSuccess) return -1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return -1;
   if (per_cu < 1) per_cu = 1;

@@ -114,7 +114,7 @@ int render(const HostScene& H, const rt_camera_settings* cs, uint64_t seed, cons
   P.stack_depth = H.max_depth > 1 ? H.max_depth : 1;
   P.n_prims = H.n_prims;
   const int variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex, H.n_instances > 0, H.leaf_kind,
-                                      rt_host_media_late(H));
+                                      rt_host_media_late(H), H.max_depth > 1 ? H.max_depth : 1);
   rt_host_plan_work(P, 4096, (variant & RT_VAR_BASE) == RT_VAR_FLAT);
   P.trav_exit_pct = H.trav_exit_pct;
   if (chunk > 0) {

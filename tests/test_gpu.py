@@ -609,6 +609,27 @@ def test_all_materials_against_oracle(gpu, oracle_mod, precision):
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("mats", [False, True])
+def test_deep_bvh_against_oracle(gpu, oracle_mod, mats, precision):
+    """A BVH 26 levels deep (spheres 8^k apart along the view axis): one 1024-lane workgroup of the
+    4-wave binary64 / 8-wave FP32 (with the metal sphere) classes cannot hold its stacks beside the
+    item sums, so the scene runs their 512-lane twins (RT_VAR_NARROW, rt_render_kernel.h)."""
+    objs = [R.lambertian(R.constantTexture(0.5)) << R.sphere((0, -1000.5, -1), 1000)]
+    for k in range(40):
+        objs.append(R.lambertian(R.constantTexture((0.8, 0.3, 0.2))) << R.sphere((0.3 * (k % 3 - 1), 0.0, -2.0 - 8.0 ** k), 0.2))
+    if mats:
+        objs.append(R.metal(0.2, R.constantTexture(0.8)) << R.sphere((0.6, 0.1, -2.5), 0.3))
+    world = R.group(objs)
+    cs = R.defaultCameraSettings(cs_imageWidth=96, cs_aspectRatio=1.5, cs_samplesPerPixel=8, cs_background=R.sky,
+                                 cs_center=(0, 0.3, 1), cs_lookAt=(0, 0, -3))
+    st = {}
+    img = R.raytrace(cs, world, R.mkStdGen(5), precision=precision, stats=st)
+    assert st["max_stack"] >= 24, st  # deeper than a 1024-lane binary64 workgroup's stacks hold
+    ref = oracle_mod.render(cs, world, R.mkStdGen(5), mode=oracle_mod.RNG_PHILOX)
+    assert_parity(img, ref, precision, 0.98, _floor()["cornell"], "deep_bvh", 8, 1.0)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
 def test_moving_and_transform_against_oracle(gpu, oracle_mod, precision):
     """`moving` (motion blur, Geometry.hs:449-456) and rotated textured spheres (sphereUV frame)."""
     tex = R.checkerTexture(8, 4, (0.9, 0.1, 0.1), (0.1, 0.1, 0.9))
