@@ -1,3 +1,7 @@
+"""Determinism check of one library build on the GPU box: installs the given librt_amd.so over the
+in-tree one (the box's copy is scratch), renders bunny_instances (FP32, 4 spp, 8 x 8 placements)
+three times and prints the frames' max difference (0 for a deterministic build) and mean.
+usage (on the GPU box): python tools/determinism_check.py <lib.so>"""
 import ctypes, os, sys, shutil, numpy as np
 sys.path.insert(0, os.getcwd())
 lib = sys.argv[1]
