@@ -353,7 +353,10 @@ struct WaveWork {
 #define RT_WAVES64_BVH_MEDIA_LATE 4  // media events in the shading phase (kMedia 2): pawn+fog 508 -> 476 ms
 #endif
 #ifndef RT_WAVES_BVH_MEDIA_LATE
-#define RT_WAVES_BVH_MEDIA_LATE 7  // FP32 pawn+fog 310.7 -> 302 ms against 5 (profiles/r5/licm)
+// FP32 pawn+fog: 310.7 -> 302 ms at 7 against 5 (profiles/r5/licm); 6, in two 768-lane workgroups
+// per CU, stages 520 of its 631 surface nodes per copy against 120 at 7: 302.7 -> 276.1 ms (4:
+// 318, 8: 297; profiles/r5/occ)
+#define RT_WAVES_BVH_MEDIA_LATE 6
 #endif
 #ifndef RT_WAVES_BVH_MATS
 #define RT_WAVES_BVH_MATS 8  // FP32 BVH, constant textures, the full material set, no media (demo1 39.7 -> 39.25 ms)
