@@ -435,7 +435,11 @@ void rt_render_kernel(KernelParams P) {
 #endif
   constexpr int kSlots = RT_AGG_SLOTS_OF(kVar), kPix = RT_AGG_PIX_OF(kVar);
   // (the launch bound; a deep BVH's render may launch fewer lanes: host render_block)
+#if defined(RT_BLOCK_RUNTIME)  // (experiment: the stack stride from blockDim; profiles/r5/bigwg)
+  const int block = (int)blockDim.x;
+#else
   constexpr int block = RT_BLOCK_N(kVar, kTex, kMedia, kMats, kInst, kNarrow);
+#endif
   constexpr int kAggBytes = AggGeom<kSlots, kPix>::kWaveBytes;
   const int waves = (int)(gridDim.x * (blockDim.x / 64));
   // wave-uniform (readfirstlane: the compiler cannot tell that threadIdx.x / 64 is), so the work

@@ -630,6 +630,20 @@ def test_deep_bvh_against_oracle(gpu, oracle_mod, mats, precision):
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("name", ["bunny_instances", "pawn_fog", "demo1"])
+def test_renders_are_deterministic(gpu, name, precision):
+    """The same frame twice is bit-identical (fixed-point sums make the image independent of the
+    schedule).  A build whose FP32 instanced kernel spilled VGPRs rendered this scene
+    nondeterministically (profiles/r5/bigwg/README.md): the check guards every kernel class the
+    bench configs and the instancing path use."""
+    kw = dict(spp=4, n=8) if name == "bunny_instances" else dict(spp=2)
+    cs, world, seed = getattr(scenes, name)(**kw)
+    a = R.raytrace(cs, world, seed, precision=precision)
+    b = R.raytrace(cs, world, seed, precision=precision)
+    assert np.array_equal(a, b, equal_nan=True), float(np.nanmax(np.abs(a - b)))
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
 def test_moving_and_transform_against_oracle(gpu, oracle_mod, precision):
     """`moving` (motion blur, Geometry.hs:449-456) and rotated textured spheres (sphereUV frame)."""
     tex = R.checkerTexture(8, 4, (0.9, 0.1, 0.1), (0.1, 0.1, 0.9))
