@@ -103,7 +103,7 @@ struct rt_device_scene {
   mutable DevArrays<double> f64;
   mutable bool have_f32 = false, have_f64 = false;
   int leaf_exit_pct = 100, leaf_exit_pct64 = 100;
-  int trav_exit_pct = 50;
+  int trav_exit_pct = 50, trav_exit_pct64 = 50;
   int surface_root = RT_EMPTY_ROOT;
   int n_media = 0;
   DevFlatSet flat_sets[1 + RT_MAX_MEDIA];
@@ -255,7 +255,7 @@ int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_
   P.n_prims = s->n_prims;
   rt_host_plan_work(P, (long long)A.resident_blocks * rt_render_block((const KernelParamsT<R>*)nullptr, s->variant),
                     (s->variant & RT_VAR_BASE) == RT_VAR_FLAT);
-  P.trav_exit_pct = s->trav_exit_pct;
+  P.trav_exit_pct = sizeof(R) == 8 ? s->trav_exit_pct64 : s->trav_exit_pct;
   P.out_frame_rows = frame_rows;
   HIP_TRY(hipSetDevice(s->device));
   // stream-ordered workspace: fixed-point sums, NaN flags, queue counter (graph-capturable)
@@ -341,6 +341,7 @@ int upload_common(const std::shared_ptr<const HostScene>& Hp, int device, rt_dev
   s->leaf_exit_pct = H.leaf_exit_pct;
   s->leaf_exit_pct64 = H.leaf_exit_pct64;
   s->trav_exit_pct = H.trav_exit_pct;
+  s->trav_exit_pct64 = H.trav_exit_pct64;
   s->n_media = H.n_media;
   for (int k = 0; k <= RT_MAX_MEDIA; ++k) s->flat_sets[k] = H.flat_sets[k];
   s->n_nodes = H.n_nodes;

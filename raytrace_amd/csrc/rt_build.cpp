@@ -856,17 +856,20 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     // the leaf tests of the BVH kernel specialised to one primitive class (rt_trace.h trav_round
     // kLeaf): bunny-Cornell 144.0 -> 139.7 ms binary64, demo1 63.9 -> 61.6 (profiles/r3/agg)
     S.leaf_kind = n == (int)prefix.size() ? 0 : static_tris ? 1 : static_spheres ? 2 : 0;
-    S.leaf_exit_pct = spheres_only ? 100 : sc->n_media > 0 ? 55 : 25;
-    // the binary64 media kernel (3 waves/SIMD, its whole pawn BVH staged in LDS) tests leaves
-    // later: pawn+fog 544.8 -> 538.7 ms at 70 % (80: 547, 40: 560); its FP32 kernel keeps 55
-    // (70: +3.6 %)
-    S.leaf_exit_pct64 = !spheres_only && sc->n_media > 0 ? 70 : S.leaf_exit_pct;
+    // With media: round 5's media kernels (shading-phase events, binary64 in one 1024-lane
+    // workgroup per CU with the whole pawn BVH staged, FP32 at 6 waves) re-swept with the lane-loop
+    // exit below (profiles/r5/policy): FP32 leaves at 40 % and lane-loop exit 50 %, pawn+fog
+    // 275.5 -> 260.5 ms; binary64 55 % and 40 %, 428.3 -> 398.9 ms (round 4: 55 / 70 and 75).
+    S.leaf_exit_pct = spheres_only ? 100 : sc->n_media > 0 ? 40 : 25;
+    S.leaf_exit_pct64 = !spheres_only && sc->n_media > 0 ? 55 : S.leaf_exit_pct;
     if (const char* e = rt_knob("RT_AMD_LEAF_EXIT_PCT"))
       S.leaf_exit_pct = S.leaf_exit_pct64 = std::max(1, std::min(100, atoi(e)));
     // and the decoupled lane loop's exit (KernelParams::trav_exit_pct): pawn+fog 386 -> 376 ms at
     // 75 %, demo1 49.2 -> 48.5 at 25 %, the bunny flat between 50 and 75
-    S.trav_exit_pct = spheres_only ? 25 : sc->n_media > 0 ? 75 : 50;
-    if (const char* e = rt_knob("RT_AMD_TRAV_PCT")) S.trav_exit_pct = std::max(0, std::min(100, atoi(e)));
+    S.trav_exit_pct = spheres_only ? 25 : sc->n_media > 0 ? 50 : 50;
+    S.trav_exit_pct64 = !spheres_only && sc->n_media > 0 ? 40 : S.trav_exit_pct;
+    if (const char* e = rt_knob("RT_AMD_TRAV_PCT"))
+      S.trav_exit_pct = S.trav_exit_pct64 = std::max(0, std::min(100, atoi(e)));
   }
   S.n_prims = n;
   return RT_OK;

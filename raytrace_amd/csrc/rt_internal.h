@@ -377,6 +377,7 @@ struct HostScene {
   int leaf_exit_pct = 100;  // BVH traversal policy for this scene (KernelParams::leaf_exit_pct)
   int leaf_exit_pct64 = 100;  // ... for the binary64 kernels
   int trav_exit_pct = 50;   // and its lane-loop exit (KernelParams::trav_exit_pct)
+  int trav_exit_pct64 = 50;  // ... for the binary64 kernels
   bool full_mats = false;  // some material is not lightSource / pitchBlack / lambertian (RT_VAR_MATS)
   int n_instances = 0;     // two-level instancing (RT_VAR_INST)
   int leaf_kind = 0;       // BVH leaves (after the prefix): 1 all static triangles, 2 all static spheres, 0 mixed

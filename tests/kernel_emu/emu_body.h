@@ -116,7 +116,7 @@ int render(const HostScene& H, const rt_camera_settings* cs, uint64_t seed, cons
   const int variant = rt_host_variant(H.flat, H.n_media, H.noise, H.full_mats, H.uv_tex, H.n_instances > 0, H.leaf_kind,
                                       rt_host_media_late(H), H.max_depth > 1 ? H.max_depth : 1);
   rt_host_plan_work(P, 4096, (variant & RT_VAR_BASE) == RT_VAR_FLAT);
-  P.trav_exit_pct = H.trav_exit_pct;
+  P.trav_exit_pct = RT_F64 ? H.trav_exit_pct64 : H.trav_exit_pct;
   if (chunk > 0) {
     P.chunk = chunk;
     P.n_chunks = (P.cam.spp + chunk - 1) / chunk;
