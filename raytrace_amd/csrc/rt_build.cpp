@@ -860,8 +860,10 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     // workgroup per CU with the whole pawn BVH staged, FP32 at 6 waves) re-swept with the lane-loop
     // exit below (profiles/r5/policy): FP32 leaves at 40 % and lane-loop exit 50 %, pawn+fog
     // 275.5 -> 260.5 ms; binary64 55 % and 40 %, 428.3 -> 398.9 ms (round 4: 55 / 70 and 75).
-    S.leaf_exit_pct = spheres_only ? 100 : sc->n_media > 0 ? 40 : 25;
-    S.leaf_exit_pct64 = !spheres_only && sc->n_media > 0 ? 55 : S.leaf_exit_pct;
+    // Sphere-only leaves: binary64 100 %; FP32 70 % since round 5 (demo1 37.73 -> 37.44 ms; binary64
+    // at 70 %: +0.6 %).
+    S.leaf_exit_pct = spheres_only ? 70 : sc->n_media > 0 ? 40 : 25;
+    S.leaf_exit_pct64 = spheres_only ? 100 : sc->n_media > 0 ? 55 : S.leaf_exit_pct;
     if (const char* e = rt_knob("RT_AMD_LEAF_EXIT_PCT"))
       S.leaf_exit_pct = S.leaf_exit_pct64 = std::max(1, std::min(100, atoi(e)));
     // and the decoupled lane loop's exit (KernelParams::trav_exit_pct): pawn+fog 386 -> 376 ms at
