@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 /* status codes */
 #define RT_OK 0
@@ -236,7 +236,9 @@ typedef struct rt_stats {
   int32_t device_allocs; /* device allocations (hipMalloc) this call made: a resident multi-device
                             scene allocates its buffers on its first render (or a larger frame)
                             only, so later rt_multi_render calls report 0 (ABI v5) */
-  int32_t pad;
+  int32_t kernel_block; /* workgroup size of the render kernel the call launched (ABI v6; the
+                           1024-lane BVH classes run a 512-lane twin for a BVH whose traversal
+                           stacks do not fit one 1024-lane workgroup's LDS); 0 from rt_scene_stats */
 } rt_stats;
 
 typedef struct rt_device_scene rt_device_scene;   /* opaque, device-resident scene */
@@ -258,7 +260,9 @@ int rt_shard_row(int32_t t, const rt_exec* ex);
 /* One-shot host-buffer call — the Haskell binding's entry point (replaces Ray.hs:121-238).
  * out_rgb: caller-owned host buffer of rt_shard_rows(h, ex) * image_width * 3 doubles (floats
  * with RT_EXEC_F32, uint8 codes with RT_EXEC_ENCODE8_*); the whole image when n_shards == 1.  Returns RT_OK or a negative RT_E_*
- * code. */
+ * code.  On RT_E_STACK a one-device call has written the partial image to out_rgb (a device list
+ * leaves it untouched); the caller renders such a scene on the CPU path.  No copy into out_rgb is
+ * in flight once the call has returned, whatever the code. */
 int rt_render(const rt_camera_settings* cs, const rt_scene* scene, uint64_t seed, const rt_exec* ex,
               void* out_rgb, rt_stats* stats);
 

@@ -58,7 +58,7 @@ RT_EXEC_F32 = 1  # rt_exec.flags: FP32 kernel, float output (default: binary64, 
 RT_EXEC_ENCODE8_SRGB = 2  # rt_render output: uint8 codes of writeImage (sRGB)
 RT_EXEC_ENCODE8_SQRT = 4  # rt_render output: uint8 codes of writeImageSqrt
 ENCODINGS = {None: 0, "srgb": RT_EXEC_ENCODE8_SRGB, "sqrt": RT_EXEC_ENCODE8_SQRT}
-ABI_VERSION = 5
+ABI_VERSION = 6
 PRECISIONS = {"f64": np.float64, "f32": np.float32}
 
 
@@ -71,7 +71,7 @@ class RtExec(ctypes.Structure):
 class RtStats(ctypes.Structure):
     _fields_ = [("upload_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
                 ("samples", ctypes.c_int64), ("bvh_nodes", ctypes.c_int32), ("max_stack", ctypes.c_int32),
-                ("device_allocs", ctypes.c_int32), ("pad", ctypes.c_int32)]
+                ("device_allocs", ctypes.c_int32), ("kernel_block", ctypes.c_int32)]
 
 
 _lib = None

@@ -499,23 +499,34 @@ int render_one(rt_multi_scene* M, const rt_camera_settings* cs, uint64_t seed, c
   if (int r = grow(&q.d_tile, &q.tile_cap, tile_pixels * 3 * esize, &allocs)) return r;
   const size_t wsb = workspace_bytes(tile_pixels, f32 ? RT_ACC_WORDS(float) : RT_ACC_WORDS(double), nullptr, nullptr);
   if (int r = grow((void**)&q.ws, &q.ws_cap, wsb, &allocs)) return r;
-  HIP_TRY(hipMemsetAsync(s->status, 0, 4 * sizeof(int), q.st));
-  HIP_TRY(hipEventRecord(q.e0, q.st));
-  const int r = f32 ? render_async<float>(s, cs, seed, &ex, (float*)q.d_tile, q.st, q.ws, q.ws_cap, 0, true)
-                    : render_async<double>(s, cs, seed, &ex, (double*)q.d_tile, q.st, q.ws, q.ws_cap, 0, true);
-  if (r) return r;
-  HIP_TRY(hipEventRecord(q.e1, q.st));
-  const void* src = q.d_tile;
-  size_t bytes = tile_pixels * 3 * esize;
-  if (encoding >= 0) {
-    const int64_t nv = (int64_t)tile_pixels * 3;
-    if (rt_launch_encode8(q.d_tile, f32 ? 0 : 1, M->d_codes, nv, encode8_table(encoding), encoding, q.st))
-      return fail(RT_E_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
-    src = M->d_codes;
-    bytes = (size_t)nv;
+  // everything below is enqueued on q.st; a failure after the first enqueue synchronises the
+  // stream before returning, so no copy into out_host is still in flight when the call returns
+  auto enqueue = [&]() -> int {
+    HIP_TRY(hipMemsetAsync(s->status, 0, 4 * sizeof(int), q.st));
+    HIP_TRY(hipEventRecord(q.e0, q.st));
+    const int r = f32 ? render_async<float>(s, cs, seed, &ex, (float*)q.d_tile, q.st, q.ws, q.ws_cap, 0, true)
+                      : render_async<double>(s, cs, seed, &ex, (double*)q.d_tile, q.st, q.ws, q.ws_cap, 0, true);
+    if (r) return r;
+    HIP_TRY(hipEventRecord(q.e1, q.st));
+    const void* src = q.d_tile;
+    size_t bytes = tile_pixels * 3 * esize;
+    if (encoding >= 0) {
+      const int64_t nv = (int64_t)tile_pixels * 3;
+      if (rt_launch_encode8(q.d_tile, f32 ? 0 : 1, M->d_codes, nv, encode8_table(encoding), encoding, q.st))
+        return fail(RT_E_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
+      src = M->d_codes;
+      bytes = (size_t)nv;
+    }
+    // (the image is copied before the status word is read, in the same synchronisation: on
+    // RT_E_STACK out_host holds the partial image, include/rt.h)
+    HIP_TRY(hipMemcpyAsync(out_host, src, bytes, hipMemcpyDeviceToHost, q.st));
+    HIP_TRY(hipMemcpyAsync(M->h_status, s->status, sizeof(int), hipMemcpyDeviceToHost, q.st));
+    return RT_OK;
+  };
+  if (const int r = enqueue()) {
+    (void)hipStreamSynchronize(q.st);
+    return r;
   }
-  HIP_TRY(hipMemcpyAsync(out_host, src, bytes, hipMemcpyDeviceToHost, q.st));
-  HIP_TRY(hipMemcpyAsync(M->h_status, s->status, sizeof(int), hipMemcpyDeviceToHost, q.st));
   HIP_TRY(hipStreamSynchronize(q.st));
   if (*M->h_status) return fail(RT_E_STACK, "BVH traversal stack overflow");
   if (stats) {
@@ -528,6 +539,8 @@ int render_one(rt_multi_scene* M, const rt_camera_settings* cs, uint64_t seed, c
     stats->bvh_nodes = s->n_nodes;
     stats->max_stack = s->max_depth;
     stats->device_allocs = allocs;
+    stats->kernel_block = f32 ? rt_render_block((const KernelParamsT<float>*)nullptr, s->variant)
+                              : rt_render_block((const KernelParamsT<double>*)nullptr, s->variant);
     stats->total_ms = build_ms + std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
   return RT_OK;
@@ -689,6 +702,8 @@ int multi_render(rt_multi_scene* M, const rt_camera_settings* cs, uint64_t seed,
     stats->bvh_nodes = M->scenes[0]->n_nodes;
     stats->max_stack = M->scenes[0]->max_depth;
     stats->device_allocs = allocs;
+    stats->kernel_block = f32 ? rt_render_block((const KernelParamsT<float>*)nullptr, M->scenes[0]->variant)
+                              : rt_render_block((const KernelParamsT<double>*)nullptr, M->scenes[0]->variant);
     stats->total_ms = build_ms + std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
   return rc;

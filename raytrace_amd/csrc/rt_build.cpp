@@ -866,9 +866,10 @@ int rt_host_build_scene(const rt_scene* sc, HostScene& S, std::string& err) {
     S.leaf_exit_pct64 = spheres_only ? 100 : sc->n_media > 0 ? 55 : S.leaf_exit_pct;
     if (const char* e = rt_knob("RT_AMD_LEAF_EXIT_PCT"))
       S.leaf_exit_pct = S.leaf_exit_pct64 = std::max(1, std::min(100, atoi(e)));
-    // and the decoupled lane loop's exit (KernelParams::trav_exit_pct): pawn+fog 386 -> 376 ms at
-    // 75 %, demo1 49.2 -> 48.5 at 25 %, the bunny flat between 50 and 75
-    S.trav_exit_pct = spheres_only ? 25 : sc->n_media > 0 ? 50 : 50;
+    // and the decoupled lane loop's exit (KernelParams::trav_exit_pct): demo1 49.2 -> 48.5 ms at 25 %
+    // (round 3), the bunny flat between 50 and 75, FP32 pawn+fog best at 50 since round 5's re-sweep
+    // (profiles/r5/policy; binary64 media scenes at 40 %, below)
+    S.trav_exit_pct = spheres_only ? 25 : 50;
     S.trav_exit_pct64 = !spheres_only && sc->n_media > 0 ? 40 : S.trav_exit_pct;
     if (const char* e = rt_knob("RT_AMD_TRAV_PCT"))
       S.trav_exit_pct = S.trav_exit_pct64 = std::max(0, std::min(100, atoi(e)));

@@ -344,10 +344,16 @@ struct WaveWork {
 #define RT_WAVES64_BVH 4  // demo1 69.9 ms vs 76.6 at 3 (profiles/r2/waves64); textured scenes, instances
 #endif
 #ifndef RT_WAVES64_BVH_MATS
-#define RT_WAVES64_BVH_MATS 5  // constant textures, the full material set (demo1): 57.0 -> 56.4 ms (profiles/r5/licm)
+// constant textures, the full material set (demo1).  Round 5 ran it at 5 (57.0 -> 56.4 ms), where
+// every leaf class of it spilled 4-14 VGPRs; round 6 keeps every dispatchable kernel spill-free
+// (tools/spill_gate.py), so 4
+#define RT_WAVES64_BVH_MATS 4
 #endif
 #ifndef RT_WAVES64_BVH_MEDIA
 #define RT_WAVES64_BVH_MEDIA 3  // the media chain kernels (pawn+fog 641 ms at 3, 883 at 4), instanced with textures / media
+#endif
+#ifndef RT_WAVES64_BVH_INST_MATS
+#define RT_WAVES64_BVH_INST_MATS 3  // instances with the full material set: 1 VGPR spilled at 4
 #endif
 #ifndef RT_WAVES64_BVH_MEDIA_LATE
 #define RT_WAVES64_BVH_MEDIA_LATE 4  // media events in the shading phase (kMedia 2): pawn+fog 508 -> 476 ms
@@ -361,19 +367,29 @@ struct WaveWork {
 #ifndef RT_WAVES_BVH_MATS
 #define RT_WAVES_BVH_MATS 8  // FP32 BVH, constant textures, the full material set, no media (demo1 39.7 -> 39.25 ms)
 #endif
+#ifndef RT_WAVES_BVH_MATS_GENERIC
+#define RT_WAVES_BVH_MATS_GENERIC 7  // ... with generic leaves: 4 VGPRs spilled at 8
+#endif
+#ifndef RT_WAVES_BVH_INST_CHAIN
+#define RT_WAVES_BVH_INST_CHAIN 4  // FP32 instances with the media query chain: 2-25 VGPRs spilled at 5
+#endif
+// kLeaf: the leaf class of the instantiation (0 generic, 1 triangles, 2 spheres; rt_trace.h trav_round)
 #if RT_F64
-#define RT_WAVES_OF(kVar, kTex, kMedia, kMats, kInst)                                              \
+#define RT_WAVES_OF(kVar, kTex, kMedia, kMats, kInst, kLeaf)                                        \
   ((kVar) == RT_VAR_FLAT ? ((kTex) == 0 && !(kMedia) && !(kMats) ? RT_WAVES64_FLAT_LITE : RT_WAVES64_FLAT) \
                          : (kInst) && ((kTex) != 0 || (kMedia) != 0) ? RT_WAVES64_BVH_MEDIA          \
+                         : (kInst) && (kMats) ? RT_WAVES64_BVH_INST_MATS                            \
                          : (kMedia) == 2 ? RT_WAVES64_BVH_MEDIA_LATE                                \
                          : (kMedia) ? RT_WAVES64_BVH_MEDIA                                          \
                          : (kTex) == 0 && !(kMats) ? RT_WAVES64_BVH_LITE                            \
                          : (kTex) == 0 && !(kInst) ? RT_WAVES64_BVH_MATS : RT_WAVES64_BVH)
 #else
-#define RT_WAVES_OF(kVar, kTex, kMedia, kMats, kInst)                                                    \
+#define RT_WAVES_OF(kVar, kTex, kMedia, kMats, kInst, kLeaf)                                              \
   ((kVar) == RT_VAR_FLAT ? ((kTex) == 2 ? RT_WAVES_FLAT_NOISE : (kTex) == 0 ? RT_WAVES_FLAT_TEX0 : RT_WAVES_FLAT) \
                          : (kMedia) == 2 ? ((kInst) ? RT_WAVES_BVH : RT_WAVES_BVH_MEDIA_LATE)             \
-                         : (kTex) == 0 && !(kMedia) && (kMats) && !(kInst) ? RT_WAVES_BVH_MATS            \
+                         : (kMedia) == 1 && (kInst) ? RT_WAVES_BVH_INST_CHAIN                             \
+                         : (kTex) == 0 && !(kMedia) && (kMats) && !(kInst)                                \
+                             ? ((kLeaf) == 0 ? RT_WAVES_BVH_MATS_GENERIC : RT_WAVES_BVH_MATS)               \
                          : ((kTex) == 0 && !(kMedia) ? RT_WAVES_BVH_LITE : RT_WAVES_BVH))
 #endif
 // Kernels built without MachineLICM (rt_kernel_nl.hip / rt_kernel64_nl.hip, compiled with
@@ -414,8 +430,8 @@ struct WaveWork {
 #define RT_BLOCK_BVH_OF(w) \
   (RT_BIG_WG && ((w) == 3 || (w) == 6) ? 768 : RT_BIG_WG && ((w) == 4 || (w) == 8) ? 1024 : RT_BLOCK_BVH)
 #endif
-#define RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst) \
-  ((kVar) == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH_OF(RT_WAVES_OF(kVar, kTex, kMedia, kMats, kInst)))
+#define RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst, kLeaf) \
+  ((kVar) == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH_OF(RT_WAVES_OF(kVar, kTex, kMedia, kMats, kInst, kLeaf)))
 // commit-aggregation slots per wave and pixels per slot of a kernel class (rt_internal.h)
 #define RT_AGG_SLOTS_OF(kVar) ((kVar) == RT_VAR_FLAT ? RT_AGG_SLOTS_FLAT : RT_AGG_SLOTS_BVH)
 #define RT_AGG_PIX_OF(kVar) ((kVar) == RT_VAR_FLAT ? RT_AGG_PIX_FLAT : RT_AGG_PIX_BVH)
@@ -423,11 +439,12 @@ struct WaveWork {
 // shading phase (RT_VAR_MEDIA_LATE; rt_trace.h media_events_late)
 // kNarrow: the 1024-lane class at 512 lanes, for a scene whose stacks do not fit one 1024-lane
 // workgroup's LDS (RT_VAR_NARROW)
-#define RT_BLOCK_N(kVar, kTex, kMedia, kMats, kInst, kNarrow) \
-  ((kNarrow) && RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst) == 1024 ? 512 : RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst))
+#define RT_BLOCK_N(kVar, kTex, kMedia, kMats, kInst, kLeaf, kNarrow)                       \
+  ((kNarrow) && RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst, kLeaf) == 1024 ? 512 \
+                                                                               : RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst, kLeaf))
 template <int kVar, int kTex, int kMedia, bool kMats, bool kInst, int kLeaf, bool kNarrow = false>
-__global__ __launch_bounds__(RT_BLOCK_N(kVar, kTex, kMedia, kMats, kInst, kNarrow))
-__attribute__((amdgpu_waves_per_eu(RT_WAVES_OF(kVar, kTex, kMedia, kMats, kInst))))
+__global__ __launch_bounds__(RT_BLOCK_N(kVar, kTex, kMedia, kMats, kInst, kLeaf, kNarrow))
+__attribute__((amdgpu_waves_per_eu(RT_WAVES_OF(kVar, kTex, kMedia, kMats, kInst, kLeaf))))
 void rt_render_kernel(KernelParams P) {
   extern __shared__ int smem[];
 #if defined(RT_WAVE_STAMPS)
@@ -438,7 +455,7 @@ void rt_render_kernel(KernelParams P) {
 #if defined(RT_BLOCK_RUNTIME)  // (experiment: the stack stride from blockDim; profiles/r5/bigwg)
   const int block = (int)blockDim.x;
 #else
-  constexpr int block = RT_BLOCK_N(kVar, kTex, kMedia, kMats, kInst, kNarrow);
+  constexpr int block = RT_BLOCK_N(kVar, kTex, kMedia, kMats, kInst, kLeaf, kNarrow);
 #endif
   constexpr int kAggBytes = AggGeom<kSlots, kPix>::kWaveBytes;
   const int waves = (int)(gridDim.x * (blockDim.x / 64));
@@ -537,6 +554,18 @@ __global__ __launch_bounds__(256) void rt_resolve_kernel(const long long* __rest
 }
 #endif
 
+#ifndef RT_LEAF_MEDIA
+#define RT_LEAF_MEDIA 1
+#endif
+// the leaf class (kLeaf) of the instantiation render_kernel_of selects for a variant: one-class
+// leaves only where render_kernel_media compiles them (the decoupled kernel without instances;
+// with media, triangle leaves and constant textures only)
+static int leaf_of(int variant) {
+  if ((variant & RT_VAR_BASE) != RT_VAR_BVH || (variant & RT_VAR_INST)) return 0;
+  if (variant & RT_VAR_MEDIA)
+    return RT_LEAF_MEDIA && !(variant & (RT_VAR_TEX | RT_VAR_NOISE)) && (variant & RT_VAR_LEAF_TRI) ? 1 : 0;
+  return (variant & RT_VAR_LEAF_TRI) ? 1 : (variant & RT_VAR_LEAF_SPHERE) ? 2 : 0;
+}
 // the workgroup of a variant's kernel (RT_BLOCK_OF of its class; RT_VAR_NARROW: half the
 // 1024-lane workgroup, rt_build.cpp rt_host_variant)
 static int render_block(int variant) {
@@ -544,7 +573,7 @@ static int render_block(int variant) {
   const int tex = (variant & RT_VAR_NOISE) ? 2 : (variant & RT_VAR_TEX) ? 1 : 0;
   const int media = RT_MEDIA_OF(variant);
   const bool mats = (variant & RT_VAR_MATS) != 0, inst = (variant & RT_VAR_INST) != 0;
-  const int b = RT_BLOCK_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats, inst);
+  const int b = RT_BLOCK_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats, inst, leaf_of(variant));
   return b == 1024 && (variant & RT_VAR_NARROW) ? 512 : b;
 }
 static bool acc_in_lds(int variant) {
@@ -572,14 +601,11 @@ static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
 // (inlined everywhere it raises the register allocation of every scene's kernel: the Cornell
 // box is 4.8 % faster without the unused media code)
 typedef void (*render_fn)(KernelParams);
-#ifndef RT_LEAF_MEDIA
-#define RT_LEAF_MEDIA 1
-#endif
 // this translation unit's instantiation, or null when the other one holds it (RT_NOLICM_OF)
 template <int kVar, int kTex, int kMedia, bool kMats, bool kInst, int kLeaf>
 static render_fn kernel_here(int variant) {
   if constexpr ((bool)(RT_NOLICM_OF(kVar, kTex, kMedia, kMats, kInst)) == (bool)RT_TU_NOLICM) {
-    if constexpr (RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst) == 1024)  // (the narrow twin)
+    if constexpr (RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst, kLeaf) == 1024)  // (the narrow twin)
       if (variant & RT_VAR_NARROW) return rt_render_kernel<kVar, kTex, kMedia, kMats, kInst, kLeaf, true>;
     return rt_render_kernel<kVar, kTex, kMedia, kMats, kInst, kLeaf, false>;
   } else {
@@ -703,7 +729,7 @@ int rt_render_waves(const KernelParamsT<RT_NS::real>*, int variant) {
   const int tex = (variant & RT_VAR_NOISE) ? 2 : (variant & RT_VAR_TEX) ? 1 : 0;
   const int media = RT_MEDIA_OF(variant);
   const bool mats = (variant & RT_VAR_MATS) != 0, inst = (variant & RT_VAR_INST) != 0;
-  return RT_WAVES_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats, inst);
+  return RT_WAVES_OF(flat ? RT_VAR_FLAT : RT_VAR_BVH, tex, media, mats, inst, RT_NS::leaf_of(variant));
 }
 int rt_render_block(const KernelParamsT<RT_NS::real>*, int variant) { return RT_NS::render_block(variant); }
 int rt_render_acc_lds(const KernelParamsT<RT_NS::real>*, int variant) {

@@ -1458,8 +1458,10 @@ RT_FN bool shade_event(const KernelParams& P, cfp prims, uint32_t pix, int sampl
   u4 w = philox(pix, (uint32_t)sample, (uint32_t)seg, RT_EV_SCATTER, P.key0, P.key1);
 #ifdef RT_HOST_EMU
   f3 newdir = mk3(RT_NAN, RT_NAN, RT_NAN);  // poison on the CPU: read only where the path goes on
+#elif defined(RT_SHADE_UNDEF)
+  f3 newdir;  // (experiment builds only: left unset on the terminating paths, as in round 5)
 #else
-  f3 newdir;  // set where the path goes on (the caller reads it only there)
+  f3 newdir = mk3(RL(0.), RL(0.), RL(0.));  // defined on every path; read only where the path goes on
 #endif
   switch (Mt.kind) {
     case 0:  // lightSource: emit, Absorb
@@ -1591,9 +1593,14 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
   const real nan = RT_NAN;
   f3 np = mk3(nan, nan, nan), nd = np, Tf = np;
   int ngid = RT_EMPTY_ROOT;
-#else
-  f3 np, nd, Tf;
+#elif defined(RT_SHADE_UNDEF)
+  f3 np, nd, Tf;  // (experiment builds only: the round-5 code, unset on the terminating paths)
   int ngid;
+#else
+  // GPU builds: every output defined on every path (constants on the terminating ones), so no
+  // lane ever carries an uninitialised value through the lane loop's divergent joins
+  f3 np = mk3(RL(0.), RL(0.), RL(0.)), nd = np, Tf = np;
+  int ngid = -1;
 #endif
   const bool term =
       shade_event<kTex, kMats, kInst>(P, prims, pix, sample, seg, tbest, best, hit_medium, R, L, T, best_inst, np, nd, Tf, ngid);

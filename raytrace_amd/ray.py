@@ -58,7 +58,8 @@ def raytrace(settings: CameraSettings, world, seed, device: int = 0, stats: dict
                            out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st)))
     if stats is not None:
         stats.update(upload_ms=st.upload_ms, kernel_ms=st.kernel_ms, total_ms=st.total_ms, samples=st.samples,
-                     bvh_nodes=st.bvh_nodes, max_stack=st.max_stack, device_allocs=st.device_allocs)
+                     bvh_nodes=st.bvh_nodes, max_stack=st.max_stack, device_allocs=st.device_allocs,
+                     kernel_block=st.kernel_block)
     return out
 
 

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
     exported = set(re.findall(r"\bT (rt_\w+)", out.stdout))
     assert set(names) <= exported
-    assert L.rt_abi_version() == _lib.ABI_VERSION == 5
+    assert L.rt_abi_version() == _lib.ABI_VERSION == 6
 
 
 def test_host_only_entry_points_without_gpu():
@@ -64,7 +64,7 @@ int main(void) {
   P(rt_camera_settings); O(rt_camera_settings, image_width); O(rt_camera_settings, background_c0);
   O(rt_camera_settings, defocus_angle); O(rt_camera_settings, redirect_targets);
   P(rt_redirect_target); P(rt_exec); O(rt_exec, flags); O(rt_exec, devices); P(rt_stats); O(rt_stats, samples);
-  O(rt_stats, device_allocs);
+  O(rt_stats, device_allocs); O(rt_stats, kernel_block);
   return 0;
 }
 """
@@ -100,6 +100,7 @@ def test_record_layouts_match_header():
     assert c["rt_exec.flags"] == _lib.RtExec.flags.offset and c["rt_exec.devices"] == _lib.RtExec.devices.offset
     assert c["rt_stats"] == ctypes.sizeof(_lib.RtStats) and c["rt_stats.samples"] == _lib.RtStats.samples.offset
     assert c["rt_stats.device_allocs"] == _lib.RtStats.device_allocs.offset
+    assert c["rt_stats.kernel_block"] == _lib.RtStats.kernel_block.offset
 
 
 def test_render_fails_loudly_without_a_device():

@@ -625,19 +625,58 @@ def test_deep_bvh_against_oracle(gpu, oracle_mod, mats, precision):
     st = {}
     img = R.raytrace(cs, world, R.mkStdGen(5), precision=precision, stats=st)
     assert st["max_stack"] >= 24, st  # deeper than a 1024-lane binary64 workgroup's stacks hold
+    # the 512-lane twin ran (the FP32 sphere-leaf class without the full material set is a 768-lane
+    # class: no twin)
+    assert st["kernel_block"] == (512 if precision == "f64" or mats else 768), st
     ref = oracle_mod.render(cs, world, R.mkStdGen(5), mode=oracle_mod.RNG_PHILOX)
     assert_parity(img, ref, precision, 0.98, _floor()["cornell"], "deep_bvh", 8, 1.0)
 
 
+def mixed_leaf_scene(width=160, spp=2):
+    """A BVH scene whose leaves mix triangles and spheres (the generic-leaf kernel classes) with the
+    full material set (metal, dielectric, mirror beside lambertian): the bunny mesh among 48
+    spheres, sky background.  Test scene, not a reference scene."""
+    mesh = scenes.load_mesh("bunny.obj")
+    center = tuple(R.midpoint(i) for i in R.boundingBox(R.triangleMesh(mesh)))
+    bunny = R.triangleMesh(R.transformVertices(R.scale(8) @ R.translate(tuple(-c for c in center)), mesh))
+    objs = [R.lambertian(R.constantTexture(0.5)) << R.sphere((0, -1000.6, 0), 1000),
+            R.lambertian(R.constantTexture((0.8, 0.6, 0.3))) << bunny]
+    for k in range(48):
+        x, z = -3.0 + 0.9 * (k % 8), -1.0 - 0.9 * (k // 8)
+        m = [R.metal(0.1 * (k % 4), R.constantTexture(0.8)), R.dielectric(1.5), R.mirror(R.constantTexture(0.9)),
+             R.lambertian(R.constantTexture((0.2, 0.4, 0.8)))][k % 4]
+        objs.append(m << R.sphere((x, -0.35, z), 0.25))
+    cs = R.defaultCameraSettings(cs_imageWidth=width, cs_aspectRatio=1.5, cs_samplesPerPixel=spp, cs_background=R.sky,
+                                 cs_center=(0, 1.2, 3), cs_lookAt=(0, 0, -2))
+    return cs, R.group(objs), R.mkStdGen(13)
+
+
+DETERMINISM_SCENES = {
+    # the instanced classes (FP32 spilled in a round-5 experiment build), the media kernels, demo1
+    "bunny_instances": lambda: scenes.bunny_instances(spp=4, n=8),
+    "pawn_fog": lambda: scenes.pawn_fog(width=200, spp=2),
+    "demo1": lambda: scenes.demo1(width=300, spp=2),
+    # classes that spilled VGPRs in the round-5 product build (profiles/r5/final/resources.txt): the
+    # full-material generic-leaf class, the instanced classes with textures and the media query
+    # chain (demo2 with RT_AMD_MEDIA_LATE=0), instances with textured leaves and the full material set
+    "mixed_leaf": mixed_leaf_scene,
+    "demo2_chain": lambda: scenes.demo2(width=160, spp=2, depth=4),
+    "instance_gallery": lambda: scenes.instance_gallery(width=160, spp=2),
+    "box_gallery": lambda: scenes.box_gallery(width=120, spp=2),
+    "noise_test": lambda: scenes.noise_test(width=160, spp=2),
+}
+
+
 @pytest.mark.parametrize("precision", ["f64", "f32"])
-@pytest.mark.parametrize("name", ["bunny_instances", "pawn_fog", "demo1"])
-def test_renders_are_deterministic(gpu, name, precision):
+@pytest.mark.parametrize("name", list(DETERMINISM_SCENES))
+def test_renders_are_deterministic(knobs, gpu, name, precision):
     """The same frame twice is bit-identical (fixed-point sums make the image independent of the
-    schedule).  A build whose FP32 instanced kernel spilled VGPRs rendered this scene
-    nondeterministically (profiles/r5/bigwg/README.md): the check guards every kernel class the
-    bench configs and the instancing path use."""
-    kw = dict(spp=4, n=8) if name == "bunny_instances" else dict(spp=2)
-    cs, world, seed = getattr(scenes, name)(**kw)
+    schedule).  A build whose FP32 instanced kernel spilled VGPRs rendered nondeterministically
+    (profiles/r5/bigwg/README.md); since round 6 no dispatchable kernel spills (tests/test_spill_gate.py)
+    and this check renders every kernel class that spilled before, and the bench configs' classes."""
+    if name == "demo2_chain":
+        knobs.setenv("RT_AMD_MEDIA_LATE", "0")
+    cs, world, seed = DETERMINISM_SCENES[name]()
     a = R.raytrace(cs, world, seed, precision=precision)
     b = R.raytrace(cs, world, seed, precision=precision)
     assert np.array_equal(a, b, equal_nan=True), float(np.nanmax(np.abs(a - b)))
