@@ -452,10 +452,26 @@ void rt_render_kernel(KernelParams P) {
 #endif
   constexpr int kSlots = RT_AGG_SLOTS_OF(kVar), kPix = RT_AGG_PIX_OF(kVar);
   // (the launch bound; a deep BVH's render may launch fewer lanes: host render_block)
-#if defined(RT_BLOCK_RUNTIME)  // (experiment: the stack stride from blockDim; profiles/r5/bigwg)
+#if defined(RT_BLOCK_RUNTIME)  // (experiment: the stack stride from blockDim; profiles/r5/bigwg, r6/nondet)
   const int block = (int)blockDim.x;
 #else
   constexpr int block = RT_BLOCK_N(kVar, kTex, kMedia, kMats, kInst, kLeaf, kNarrow);
+#endif
+  // (experiments, profiles/r6/nondet: one use of the launch-time workgroup size at a time)
+#if defined(RT_BLOCK_RUNTIME_STACK)
+  const int block_stack = (int)blockDim.x;
+#else
+  const int block_stack = block;
+#endif
+#if defined(RT_BLOCK_RUNTIME_NODES)
+  const int block_nodes = (int)blockDim.x;
+#else
+  const int block_nodes = block;
+#endif
+#if defined(RT_BLOCK_RUNTIME_COPY)
+  const int block_copy = (int)blockDim.x;
+#else
+  const int block_copy = block;
 #endif
   constexpr int kAggBytes = AggGeom<kSlots, kPix>::kWaveBytes;
   const int waves = (int)(gridDim.x * (blockDim.x / 64));
@@ -497,15 +513,15 @@ void rt_render_kernel(KernelParams P) {
     work.finish();
     RT_STAMP_END(work)
   } else {
-    v4f* lds_nodes = reinterpret_cast<v4f*>(smem_rest + (P.stack_depth + 1) * block);
+    v4f* lds_nodes = reinterpret_cast<v4f*>(smem_rest + (P.stack_depth + 1) * block_nodes);
     const float4* src = reinterpret_cast<const float4*>(P.nodes);
-    for (int i = threadIdx.x; i < 4 * P.lds_nodes; i += block) {
+    for (int i = threadIdx.x; i < 4 * P.lds_nodes; i += block_copy) {
       const float4 q = src[i];
       lds_nodes[i] = v4f{q.x, q.y, q.z, q.w};
     }
     __syncthreads();
     WaveWork<kSlots, kPix, RT_KARGS_WORK_BVH> work(P, wave, waves, agg);
-    const Trav W{smem_rest + threadIdx.x, block, lds_nodes};
+    const Trav W{smem_rest + threadIdx.x, block_stack, lds_nodes};
     if constexpr (kVar == RT_VAR_BVH_LOCKSTEP)
       overflow = lane_loop_lockstep<false, kTex, kMedia != 0, kMats>(P, work, W, P.prims, acc);
     else

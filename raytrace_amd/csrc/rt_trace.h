@@ -359,6 +359,8 @@ RT_FN u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
 }
 // [0, 1) with 24 random bits: exact in both FP32 and the oracle's FP64
 RT_FN real u01(uint32_t w) { return (real)(w >> 8) * (RL(1.0) / RL(16777216.0)); }
+// (assembling m 2^-24 and a + m 2^-24 from binary64 bit patterns instead of the conversions spilled
+// the binary64 Cornell kernel and ran 0.5-2 % slower: profiles/r6/flat)
 
 // uniform direction on the unit sphere (the distribution of randomUnitVector, Core.hs:54-60)
 RT_FN f3 unit_vector(uint32_t a, uint32_t b) {
@@ -930,7 +932,8 @@ RT_FN void acc_add(Acc& A, int c, real x, bool& bad) {
     return;
   }
   // (the same words from 32-bit conversions only, floor(x) 2^32 + floor(frac(x) 2^32), measured no
-  // faster: Cornell 4.887 vs 4.889 ms, pawn+fog +1 %; profiles/r5/variants)
+  // faster: Cornell 4.887 vs 4.889 ms, pawn+fog +1 %; profiles/r5/variants.  From the low words of
+  // integer-valued binary64 plus 1.5 2^52, no conversions: Cornell +1.4 %, profiles/r6/flat)
   const real xs = x * RL(4294967296.0);
   const real fl = RFLOOR(xs);
   A.hi[c] += (long long)fl;
@@ -1072,6 +1075,19 @@ RT_FN bool trav_done(const TravState& S) { return S.node == RT_EMPTY_ROOT && S.l
 #ifndef RT_NODE_SADDR
 #define RT_NODE_SADDR (!RT_F64)
 #endif
+// The word offset of a stack row.  (Experiments, profiles/r6/nondet: RT_STACK_ASM_NOP computes it
+// with v_mul_lo_u32 in inline assembly followed by wait states, to test a multiply -> LDS-address
+// hazard in the runtime-stride builds that rendered nondeterministically.)
+#if defined(RT_STACK_ASM_NOP) && !defined(RT_HOST_EMU)
+RT_FN int stack_row_asm(int row, int stride) {
+  int off;
+  asm volatile("v_mul_lo_u32 %0, %1, %2\n\ts_nop 7\n\ts_nop 7" : "=v"(off) : "v"(row), "s"(stride));
+  return off;
+}
+#define RT_STACK_ROW(row, stride) stack_row_asm((row), (stride))
+#else
+#define RT_STACK_ROW(row, stride) ((row) * (stride))
+#endif
 // One while-while round: descend until this lane (and the wave) holds a leaf, then test leaves.
 // kInst (two-level instancing): a child RT_INST_FLAG | k enters placement k — the lane's ray R
 // is moved to object space, RT_INST_EXIT is pushed and the object's BVH is traversed; popping
@@ -1088,7 +1104,7 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
   auto pop = [&]() -> int {
     if (S.sp == 0) return kDone;
     --S.sp;
-    return stack[S.sp * stride];
+    return stack[RT_STACK_ROW(S.sp, stride)];
   };
   while (S.node >= 0) {
     RT_PROF_PADD(PF_NODE_STEPS, 1);
@@ -1111,7 +1127,7 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
           const int k = S.node - RT_INST_FLAG;
           const RT_CAS DevInstance* I = inst_rec(P, k);
           if (S.sp < P.stack_depth) {
-            stack[S.sp * stride] = RT_INST_EXIT;
+            stack[RT_STACK_ROW(S.sp, stride)] = RT_INST_EXIT;
             ++S.sp;
           } else {
             overflow = 1;  // the stack is sized for world + object levels (rt_build.cpp): not reached
@@ -1187,10 +1203,10 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
       const int nearc = both ? (rfirst ? cr : cl) : (hl ? cl : cr);
       const int farc = rfirst ? cl : cr;
       const int sp = S.sp;
-      const int top1 = stack[(sp > 0 ? sp - 1 : 0) * stride];
-      const int top2 = stack[(sp > 1 ? sp - 2 : 0) * stride];
+      const int top1 = stack[RT_STACK_ROW(sp > 0 ? sp - 1 : 0, stride)];
+      const int top2 = stack[RT_STACK_ROW(sp > 1 ? sp - 2 : 0, stride)];
       const bool room = sp < P.stack_depth;
-      stack[(room ? sp : P.stack_depth) * stride] = farc;
+      stack[RT_STACK_ROW(room ? sp : P.stack_depth, stride)] = farc;
       overflow |= (both && !room) ? 1 : 0;
       int next = (both || one) ? nearc : (sp > 0 ? top1 : kDone);
       int nsp = both ? (room ? sp + 1 : sp) : one ? sp : (sp > 0 ? sp - 1 : 0);
@@ -1461,7 +1477,10 @@ RT_FN bool shade_event(const KernelParams& P, cfp prims, uint32_t pix, int sampl
 #elif defined(RT_SHADE_UNDEF)
   f3 newdir;  // (experiment builds only: left unset on the terminating paths, as in round 5)
 #else
-  f3 newdir = mk3(RL(0.), RL(0.), RL(0.));  // defined on every path; read only where the path goes on
+  // defined on every path (read only where the path goes on): the incoming direction on the
+  // terminating ones, a value already in registers, so the join needs no copies
+  f3 newdir = R.d;
+  Tf = tex;
 #endif
   switch (Mt.kind) {
     case 0:  // lightSource: emit, Absorb
@@ -1597,10 +1616,13 @@ RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int
   f3 np, nd, Tf;  // (experiment builds only: the round-5 code, unset on the terminating paths)
   int ngid;
 #else
-  // GPU builds: every output defined on every path (constants on the terminating ones), so no
-  // lane ever carries an uninitialised value through the lane loop's divergent joins
-  f3 np = mk3(RL(0.), RL(0.), RL(0.)), nd = np, Tf = np;
-  int ngid = -1;
+  // GPU builds: every output defined on every path, so no lane carries an uninitialised value
+  // through the lane loop's divergent joins.  A miss keeps the incoming ray (and throughput
+  // factor 1); shade_event's terminating paths set the hit point, the incoming direction and the
+  // texture colour — values already in registers (constants here cost ~40 copies per iteration
+  // of the flat binary64 loop, 3 % of the Cornell frame)
+  f3 np = R.o, nd = R.d, Tf = mk3(RL(1.), RL(1.), RL(1.));
+  int ngid = R.self_gid;
 #endif
   const bool term =
       shade_event<kTex, kMats, kInst>(P, prims, pix, sample, seg, tbest, best, hit_medium, R, L, T, best_inst, np, nd, Tf, ngid);

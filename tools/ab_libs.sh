@@ -8,7 +8,7 @@ OUT=gpurun_out/$TAG; mkdir -p $OUT
 for cfg in $CFGS; do
   n=${cfg%%:*}; sh=${cfg#*:}
   for rep in $(seq 1 ${REPS:-1}); do
-  for lib in base raytrace_amd/_lib/exp/*.so; do
+  for lib in base ${LIBS:-raytrace_amd/_lib/exp/*.so}; do
     nm=$(basename $lib .so); [ ${REPS:-1} -gt 1 ] && nm=${nm}_r$rep
     if [ "$lib" = base ]; then unset RT_AMD_LIB; else export RT_AMD_LIB=$PWD/$lib; fi
     timeout -k 10 200 python bench.py --no-cpu-baseline --no-f32 --precision ${PREC:-f64} --config $n --steps $STEPS --sim-shards $sh > $OUT/${n}_${sh}_$nm.json 2>>$OUT/err.log || { echo "$nm failed"; exit 1; }
