@@ -7,9 +7,10 @@
 One step = one full frame of the config (Cornell box 600x600, 200 spp, depth 50, redirect
 target, seed 234 — test/Main.hs:188-218) with the scene already resident in HBM.  With N
 ranks (one process per GPU) the frame's rows are dealt to ranks round-robin (--row-block 1)
-(rt_exec row interleave) and the framebuffer tiles are gathered over RCCL (all_gather into one
-tensor) inside the timed region — asynchronously, so frame i+1 renders while frame i's gather is in
-flight (two frame buffers); the clock stops after every frame is rendered AND gathered.
+(rt_exec row interleave) and the framebuffer tiles are gathered to rank 0 over RCCL (one gather
+into rank 0's frame) inside the timed region — asynchronously, so frame i+1 renders
+while frame i's gather is in flight (two frame buffers); the clock stops after every frame is
+rendered AND gathered.
 `value` = pixels x spp of all ranks / max-over-ranks time.
 The W warm-up frames are followed by more untimed frames until the warm-up has rendered for
 --warmup-s seconds (2 by default: the per-frame time only settles after a few hundred ms of
@@ -301,7 +302,6 @@ def main():
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"],
                     help="the kernel precision of the line's value (f64: the reference's binary64)")
     ap.add_argument("--no-f32", action="store_true", help="skip the FP32 fast-path record after an f64 line")
-    ap.add_argument("--check", action="store_true", help="gather + assemble + sanity-check the frame after timing")
     ap.add_argument("--streams", type=int, default=0, choices=[0, 1, 2, 3, 4],
                     help="frames alternate between this many HIP streams (2: frame i+1 fills the CUs that "
                          "frame i's last long paths leave idle); 0 = auto: 2 for flat scenes, 1 for BVH "
@@ -389,7 +389,9 @@ def main():
         # buffers frame i+2 would wait for that gather and leave frame i+1's tail alone on the CUs
         nbuf = args.streams + (1 if n > 1 and args.streams > 1 else 0) + (1 if n > 1 and args.streams == 1 else 0)
         tiles = [torch.empty((rows, w, 3), dtype=dtype, device=dev) for _ in range(nbuf)]
-        gathered = [torch.empty((n * rows, w, 3), dtype=dtype, device=dev) for _ in range(nbuf)] if n > 1 else None
+        # the frame buffers the tiles are gathered into: rank 0 only (the gather's destination)
+        gathered = ([torch.empty((n * rows, w, 3), dtype=dtype, device=dev) for _ in range(nbuf)]
+                    if n > 1 and rank == 0 else None)
         works = [None] * nbuf
         streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(args.streams - 1)]
         ev = []
@@ -421,7 +423,10 @@ def main():
                 ev.append((e0, e1))
             if n > 1:
                 if args.dist_backend == "nccl":
-                    works[b] = dist.all_gather_into_tensor(gathered[b], tile, async_op=True)
+                    # every rank's tile into rank 0's frame (a gather, not an all-gather;
+                    # RCCL point-to-point over each rank's xGMI link to GPU 0)
+                    parts = list(gathered[b].chunk(n)) if rank == 0 else None
+                    works[b] = dist.gather(tile, gather_list=parts, dst=0, async_op=True)
                     if timed:
                         with torch.cuda.stream(probe):
                             works[b].wait()
@@ -429,9 +434,10 @@ def main():
                             g.record(probe)
                         gev.append((e1, g))
                 else:  # rehearsal path: through host memory
-                    parts = [torch.empty((rows, w, 3), dtype=dtype) for _ in range(n)]
-                    dist.all_gather(parts, tile.cpu())
-                    gathered[b].copy_(torch.cat(parts).to(dev))
+                    parts = [torch.empty((rows, w, 3), dtype=dtype) for _ in range(n)] if rank == 0 else None
+                    dist.gather(tile.cpu(), gather_list=parts, dst=0)
+                    if rank == 0:
+                        gathered[b].copy_(torch.cat(parts).to(dev))
 
         def drain():
             for k in range(nbuf):
@@ -486,7 +492,7 @@ def main():
             span = max(ev[0][0].elapsed_time(b) for _, b in ev[-len(streams):])
             kernel_ms = span / len(ev)
         check = None
-        if args.check or rank == 0:
+        if rank == 0:  # (the frame exists on rank 0 only)
             import numpy as np
             last = (frame[0] - 1) % nbuf
             if n > 1:
@@ -515,7 +521,7 @@ def main():
                      "slowest_rank_wall": max(allr, key=lambda r: r["ms_per_step_local"])["rank"],
                      "slowest_rank_kernel": max(allr, key=lambda r: r["kernel_ms"])["rank"],
                      "note": "kernel_ms: the rank's render device time per frame (HIP events); gather_after_render_ms: "
-                             "a frame's render end -> its RCCL all_gather done (probe stream, RCCL only); "
+                             "a frame's render end -> its RCCL gather to rank 0 done on this rank (probe stream, RCCL only); "
                              "ms_per_step_local: the rank's own timed region / frames before the max over ranks"}
         return dict(elapsed=elapsed, launch_ms=launch_ms, kernel_ms=kernel_ms, warm_frames=warm_frames,
                     warm_s=warm_s, check=check, streams=len(streams), ranks=ranks)
@@ -557,7 +563,7 @@ def main():
             "config": {"workload": f"{args.config} {w}x{h} {spp}spp depth {cs.cs_maxRecursionDepth}",
                        "width": w, "height": h, "spp": spp, "max_depth": cs.cs_maxRecursionDepth,
                        "parallelism": f"rows interleaved over {n} GPU(s), row_block {args.row_block}"
-                                      + ((", RCCL all_gather of the framebuffer" if args.dist_backend == "nccl"
+                                      + ((", RCCL gather of the framebuffer to rank 0" if args.dist_backend == "nccl"
                                           else ", gloo gather through host memory (rehearsal)") if n > 1 else "")
                                       + (f" (diagnostic: shard 0 of {n_sh} only)" if n_sh != n else "")},
             "roofline": main_rec["roofline"], "cpu_baseline": cpu, "check": main_rec["check"],

@@ -53,7 +53,7 @@ module Graphics.Ray.Device
   , Texture(Texture), constantTexture, solidTexture, uvTexture, imageTexture, checkerTexture, noiseTexture
   , marbleTexture
     -- * Between the reference's values and these
-  , toReference, referenceMaterial, referenceTexture
+  , toReference, toReferenceRandom, referenceMaterial, referenceTexture
   , fromReferenceGeometry, fromReferenceMaterial, fromReferenceTexture
     -- * Unchanged from the reference
   , R.CameraSettings(..), R.defaultCameraSettings, R.ToRandom, R.Mesh(R.Mesh), R.transformVertices, R.parseObj
@@ -185,6 +185,15 @@ fromReferenceTexture = DeviceTexture Nothing
 -- | The reference geometry with the reference materials (what 'R.raytrace' takes).
 toReference :: Functor m => Geometry m Material -> R.Geometry m R.Material
 toReference = fmap matRef . geoRef
+
+-- | The same, with its hit function lifted into 'State StdGen' by the reference's own
+-- 'R.toRandom' — exactly what 'R.raytrace' applies to every hit (Ray.hs:178; for
+-- @State StdGen@ its 'R.toRandom' is 'id'), so @R.raytrace cs (toReferenceRandom w)@ draws the
+-- same numbers as @R.raytrace cs (toReference w)@ and the CPU fallback needs no constraint beyond
+-- the reference's own @ToRandom m@ (Ray.hs:121).
+toReferenceRandom :: R.ToRandom m => Geometry m Material -> R.Geometry (State StdGen) R.Material
+toReferenceRandom g = case geoRef g of
+  R.Geometry box hit -> R.Geometry box (\t r i -> fmap (fmap (fmap matRef)) (R.toRandom (hit t r i)))
 
 referenceMaterial :: Material -> R.Material
 referenceMaterial = matRef
@@ -867,14 +876,14 @@ renderImage8 opts enc settings world gen = do
 -- what @writeImage path (raytrace cs world gen)@ writes (Sqrt: writeImageSqrt), with the 8-bit
 -- encoding done on the GPU; scenes the device cannot render go through the reference's CPU
 -- raytrace and writer.
-raytraceToFile :: (R.ToRandom m, Functor m) => Encoding -> FilePath -> R.CameraSettings -> Geometry m Material
+raytraceToFile :: R.ToRandom m => Encoding -> FilePath -> R.CameraSettings -> Geometry m Material
                -> StdGen -> IO ()
 raytraceToFile enc path settings world gen = do
   r <- renderImage8 defaultDeviceOptions enc settings world gen
   case r of
     Right codes -> I.writeImageAuto path (A.map toPixel codes)
     Left e | fallback e -> (if enc == SRGB then R.writeImage else R.writeImageSqrt) path
-                             (R.raytrace settings (toReference world) gen)
+                             (R.raytrace settings (toReferenceRandom world) gen)
            | otherwise -> ioError (userError ("Graphics.Ray.Device.raytraceToFile: " ++ show e))
   where
     -- the codes are already the stored 8-bit values: written as non-linear sRGB bytes, unconverted
@@ -891,16 +900,16 @@ fallback (LibraryError code _) = code == -3 || code == -5
 -- | 'Graphics.Ray.raytrace' on the GPU: same arguments, same result (Ray.hs:121-238).  Falls
 -- back to the reference's CPU path when the scene is not reifiable or the library reports
 -- RT_E_UNSUPPORTED or RT_E_STACK; any other library error (no device, a HIP failure) is raised.
--- The constraint adds `Functor m` to the reference's `ToRandom m` (the CPU fallback maps the
--- reference materials over the geometry); every geometry monad (Identity, State StdGen) is one.
-raytrace :: (R.ToRandom m, Functor m) => R.CameraSettings -> Geometry m Material -> StdGen -> A.Matrix A.D Color
+-- The signature is the reference's (Ray.hs:121): the CPU fallback lifts the geometry into
+-- 'State StdGen' through 'R.toRandom' ('toReferenceRandom') instead of mapping inside @m@.
+raytrace :: R.ToRandom m => R.CameraSettings -> Geometry m Material -> StdGen -> A.Matrix A.D Color
 raytrace = raytraceWith defaultDeviceOptions
 
-raytraceWith :: (R.ToRandom m, Functor m) => DeviceOptions -> R.CameraSettings -> Geometry m Material -> StdGen
+raytraceWith :: R.ToRandom m => DeviceOptions -> R.CameraSettings -> Geometry m Material -> StdGen
              -> A.Matrix A.D Color
 raytraceWith opts settings world gen =
   case unsafePerformIO (renderOnDevice opts settings world gen) of
     Right img -> A.delay img
-    Left e | fallback e -> R.raytrace settings (toReference world) gen
+    Left e | fallback e -> R.raytrace settings (toReferenceRandom world) gen
            | otherwise -> error ("Graphics.Ray.Device.raytrace: rt_render failed: " ++ show e)
 {-# NOINLINE raytraceWith #-}

@@ -1,11 +1,13 @@
-"""Multi-GPU rendering: one process per GPU, rows dealt to ranks, framebuffer gathered over RCCL.
+"""Multi-GPU rendering: one process per GPU, rows dealt to ranks, framebuffer gathered to rank 0
+over RCCL.
 
 Pixels are independent (Ray.hs:238) and the Philox stream is keyed by the GLOBAL pixel index,
 so any row partition renders exactly the image a single GPU renders.  Rank r owns the rows
 {y : (y / row_block) % world_size == r} (interleaved blocks balance the uneven per-row cost of
-a scene); every rank's tile has the same padded row count, so the exchange is a single
-all_gather_into_tensor of equal-size tiles (0.9 MB per rank at 600x600 on 8 GPUs) — the only
-collective on the path.  Rank 0 un-permutes the rows.
+a scene); every rank's tile has the same padded row count, so the exchange is one gather of
+equal-size tiles to rank 0 (torch.distributed.gather: RCCL point-to-point sends into
+rank 0's frame, 0.9 MB per rank at 600x600 on 8 GPUs, each over its own xGMI link) — the only
+collective on the path.  Only rank 0 holds the frame; it un-permutes the rows.
 
 `tile_fn` lets the CPU tests drive the same partition / gather / assembly logic over `gloo`
 with a host renderer; the product path renders on the local GPU through DeviceScene.
@@ -44,7 +46,9 @@ class ShardedRenderer:
             self.scene = None
             self.world = world
         self.tile = torch.empty((self.rows, self.w, 3), dtype=dtype, device=self.device)
-        self.gathered = torch.empty((self.world_size * self.rows, self.w, 3), dtype=dtype, device=self.device)
+        # the frame: rank 0 only (a gather's destination); the tiles land in consecutive row blocks
+        self.gathered = (torch.empty((self.world_size * self.rows, self.w, 3), dtype=dtype, device=self.device)
+                         if self.rank == 0 else None)
 
     def render_tile(self, seed, stream=None):
         """Enqueue (GPU) or compute (tile_fn) this rank's rows into self.tile."""
@@ -57,26 +61,35 @@ class ShardedRenderer:
         self.scene.render_async(self.settings, seed, self.tile.data_ptr(), s.cuda_stream, n_shards=self.world_size,
                                 shard=self.rank, row_block=self.row_block, precision=self.precision)
 
-    def gather(self):
+    def gather(self, async_op=False):
+        """Every rank's tile into rank 0's frame (views of it: no copy after the receive)."""
         if self.world_size > 1:
-            self.dist.all_gather_into_tensor(self.gathered, self.tile, group=self.group)
-        else:
-            self.gathered.copy_(self.tile)
+            parts = list(self.gathered.chunk(self.world_size)) if self.rank == 0 else None
+            return self.dist.gather(self.tile, gather_list=parts, dst=self._dst(), group=self.group, async_op=async_op)
+        self.gathered.copy_(self.tile)
+        return None
+
+    def _dst(self):
+        # the global rank of the group's rank 0 (torch.distributed.gather takes a global rank)
+        return self.dist.get_global_rank(self.group, 0) if self.group is not None else 0
 
     def step(self, seed, stream=None):
         self.render_tile(seed, stream)
         self.gather()
 
     def image(self) -> np.ndarray:
-        """The assembled (height, width, 3) image (valid on every rank after gather())."""
+        """The assembled (height, width, 3) image (rank 0, after gather())."""
+        if self.gathered is None:
+            raise RuntimeError("the frame is gathered to rank 0 only")
         tiles = self.gathered.view(self.world_size, self.rows, self.w, 3).cpu().numpy()
         return assemble_shards(tiles, self.h, self.row_block)
 
-    def render(self, seed) -> np.ndarray:
+    def render(self, seed):
+        """The frame (rank 0) or None (the other ranks)."""
         self.step(seed)
         if self.tile_fn is None:
             self.torch.cuda.synchronize(self.device)
-        return self.image()
+        return self.image() if self.rank == 0 else None
 
     def close(self):
         if self.scene is not None:

@@ -1,7 +1,7 @@
 """Multi-rank path on CPU: world_size 2 (and 3) over gloo.  Each rank renders its interleaved
-rows with the host build of the kernel logic, the tiles are all-gathered and un-permuted, and
-the result must equal a single-process render bit for bit (the Philox stream is keyed by the
-global pixel index)."""
+rows with the host build of the kernel logic, the tiles are gathered to rank 0 and un-permuted,
+and the result must equal a single-process render bit for bit (the Philox stream is keyed by the
+global pixel index).  Only rank 0 holds the frame."""
 import os
 import socket
 
@@ -40,6 +40,8 @@ def _worker(rank, world, port, row_block, out_path):
     img = sr.render(seed)
     if rank == 0:
         np.save(out_path, img)
+    else:
+        assert img is None and sr.gathered is None  # the gather's destination is rank 0 alone
     dist.barrier()
     dist.destroy_process_group()
 

@@ -7,7 +7,7 @@
 OUT=gpurun_out/${1:-rehearse}; mkdir -p $OUT
 CFG=${2:-cornell}
 export TMPDIR=/tmp
-ARGS="--config $CFG --steps 3 --warmup 1 --warmup-s 0.2 --no-cpu-baseline --no-f32 --check"
+ARGS="--config $CFG --steps 3 --warmup 1 --warmup-s 0.2 --no-cpu-baseline --no-f32"
 timeout -k 10 300 python bench.py $ARGS > $OUT/n1.json 2> $OUT/n1.err || { echo "n1 failed"; tail -5 $OUT/n1.err; exit 1; }
 for N in ${NS:-2 3}; do
   RT_BENCH_ONE_DEVICE=1 timeout -k 10 300 python bench.py --gpus $N $ARGS > $OUT/n$N.json 2> $OUT/n$N.err || { echo "n$N failed"; tail -20 $OUT/n$N.err; exit 1; }

@@ -44,7 +44,7 @@ def frame_stats(raw: np.ndarray) -> dict:
     bins = 10
     edges = np.linspace(0, span, bins + 1)
     alive = [float(np.mean((start < edges[i + 1]) & (end > edges[i]))) for i in range(bins)]
-    xcc = (st[:, 3] >> 32) & 0xF
+    xcc = st[:, 3] & 0xF  # HW_REG 20 (XCC_ID) in the low word; the high word is HW_ID
     return {
         "waves": int(st.shape[0]),
         "span_ms": round(span * TICK_MS, 4),
