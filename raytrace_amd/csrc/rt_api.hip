@@ -183,7 +183,7 @@ int ensure_precision(const rt_device_scene* s) {
     const int per_cu = std::max(1, 4 * waves * 64 / block);
     const int budget = (163840 / per_cu / 1024) * 1024 - 1024;
     const int used = rt_render_acc_lds((const KernelParamsT<R>*)nullptr, s->variant) +
-                     (s->stack_depth + 1 + RT_STACK_EXTRA_ROWS) * block * (int)sizeof(int);
+                     (s->stack_depth + 1) * block * (int)sizeof(int);
     A.lds_nodes = std::max(0, std::min(s->host->surface_nodes, (budget - used) / 64));
     if (const char* e = rt_knob("RT_AMD_LDS_NODES")) A.lds_nodes = std::min(A.lds_nodes, std::max(0, atoi(e)));
   }

@@ -883,7 +883,7 @@ int rt_host_variant(bool flat, int n_media, bool noise, bool mats, bool tex, boo
   int v = flat ? RT_VAR_FLAT : RT_VAR_BVH;
   // the BVH kernels' 1024-lane classes (rt_render_kernel.h RT_BLOCK_BVH_OF) hold RT_WIDE_STACK_ROWS
   // stack rows per lane; a deeper BVH takes the 512-lane twin of its class
-  const int narrow = !flat && stack_depth + 1 + RT_STACK_EXTRA_ROWS > RT_WIDE_STACK_ROWS ? RT_VAR_NARROW : 0;
+  const int narrow = !flat && stack_depth + 1 > RT_WIDE_STACK_ROWS ? RT_VAR_NARROW : 0;
   // media events in the shading phase; env RT_AMD_MEDIA_LATE=0 keeps them in the traversal loop's
   // query chain (A/B, tests: the images are bit-identical)
   if (const char* e = rt_knob("RT_AMD_MEDIA_LATE")) media_late = media_late && atoi(e) != 0;

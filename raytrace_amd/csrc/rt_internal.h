@@ -119,13 +119,6 @@
 // The deepest stack (rows) one 1024-lane workgroup holds beside its lanes' item sums and slots
 // (binary64: 48 + 16 B per lane; the FP32 classes take the same rule): deeper BVHs run RT_VAR_NARROW
 #define RT_WIDE_STACK_ROWS 23
-// LDS rows beyond the stack's (stack_depth + 1): the prim-parallel leaf experiment's per-wave
-// rank -> lane table (rt_trace.h leaf_round_parallel, -DRT_LEAF_PARALLEL)
-#if defined(RT_LEAF_PARALLEL)
-#define RT_STACK_EXTRA_ROWS 1
-#else
-#define RT_STACK_EXTRA_ROWS 0
-#endif
 // Experiment knobs (rt_build.cpp): the library reads its RT_AMD_* tuning variables (variant,
 // chunking, aggregation, prefix, box groups, LDS staging, ...) only when RT_AMD_EXPERIMENTS is set
 // to a nonzero value — A/B sessions and the tests that compare code paths set it.  Otherwise

@@ -513,7 +513,7 @@ void rt_render_kernel(KernelParams P) {
     work.finish();
     RT_STAMP_END(work)
   } else {
-    v4f* lds_nodes = reinterpret_cast<v4f*>(smem_rest + (P.stack_depth + 1 + RT_STACK_EXTRA_ROWS) * block_nodes);
+    v4f* lds_nodes = reinterpret_cast<v4f*>(smem_rest + (P.stack_depth + 1) * block_nodes);
     const float4* src = reinterpret_cast<const float4*>(P.nodes);
     for (int i = threadIdx.x; i < 4 * P.lds_nodes; i += block_copy) {
       const float4 q = src[i];
@@ -607,8 +607,7 @@ static size_t render_fixed_lds(int variant) {
 static size_t render_lds_bytes(int stack_depth, int variant, int lds_nodes) {
   return render_fixed_lds(variant) + ((variant & RT_VAR_BASE) == RT_VAR_FLAT
                     ? 0
-                    : (size_t)(stack_depth + 1 + RT_STACK_EXTRA_ROWS) * render_block(variant) * sizeof(int) +
-                          (size_t)lds_nodes * 64);
+                    : (size_t)(stack_depth + 1) * render_block(variant) * sizeof(int) + (size_t)lds_nodes * 64);
 }
 
 // the kernel instantiation of a variant code (base variant | RT_VAR_TEX | RT_VAR_NOISE |

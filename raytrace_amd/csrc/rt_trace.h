@@ -1088,78 +1088,6 @@ RT_FN int stack_row_asm(int row, int stride) {
 #else
 #define RT_STACK_ROW(row, stride) ((row) * (stride))
 #endif
-#if defined(RT_LEAF_PARALLEL) && !defined(RT_HOST_EMU)
-// (Experiment, profiles/r6/leafpar: the verdict's prim-parallel leaf tests.)  The leaf phase of a
-// traversal round with the wave's lanes as workers: every lane that holds a parked leaf of static
-// triangles (at most 2 per leaf in mesh BVHs) publishes its (lane, k) pairs; the i-th pair goes to
-// the wave's i-th active lane, which pulls the holder's ray and interval through ds_bpermute, loads
-// the record and tests it; the holder pulls its pairs' (t, margin, order) back and keeps the
-// closest by its (t, order) key — the order-independent minimum the serial loop computes.  Rows:
-// the stack's spare row (written only on overflow, an RT_E_STACK render) holds the pair table,
-// one extra row (RT_STACK_EXTRA_ROWS) the active rank -> lane table.  Wave-collective: every
-// tracing lane calls it.
-template <class RC>
-RT_FN void leaf_round_parallel(const KernelParams& P, RC& R, TravState& S, const Trav& W, int (*pop_fn)(TravState&, const Trav&)) {
-  const int lane = (int)__lane_id();
-  int* const row_pairs = W.stack - lane + P.stack_depth * W.stride;
-  int* const row_lanes = W.stack - lane + (P.stack_depth + 1) * W.stride;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  for (;;) {
-    const bool hold = S.leaf < 0;
-    const unsigned long long act = __ballot(true);
-    const unsigned long long m1 = __ballot(hold);
-    if (m1 == 0ull) break;
-    const int enc = hold ? ~S.leaf : 0;
-    const int first = enc >> RT_LEAF_SHIFT, cnt = hold ? (enc & ((1 << RT_LEAF_SHIFT) - 1)) + 1 : 0;
-    const unsigned long long m2 = __ballot(hold && cnt >= 2);
-    const int n_act = (int)__popcll(act), rank = (int)__popcll(act & lt);
-    const int off = (int)(__popcll(m1 & lt) + __popcll(m2 & lt));
-    const int total = (int)(__popcll(m1) + __popcll(m2));
-    row_lanes[rank] = lane;
-    for (int base = 0; base < total; base += n_act) {  // (wave-uniform)
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int p = off + k - base;
-        if (k < cnt && p >= 0 && p < n_act) row_pairs[p] = lane << 1 | k;
-      }
-      const bool work = base + rank < total;
-      const int hk = work ? row_pairs[rank] : lane << 1;
-      const int h = hk >> 1, kw = hk & 1;
-      // the holder's ray and query
-      RC Rh = R;
-      Rh.o = mk3(__shfl(R.o.x, h), __shfl(R.o.y, h), __shfl(R.o.z, h));
-      Rh.d = mk3(__shfl(R.d.x, h), __shfl(R.d.y, h), __shfl(R.d.z, h));
-      Rh.self_gid = __shfl(R.self_gid, h);
-      const real tmin_up = __shfl(S.tmin_up, h);
-      const int first_h = __shfl(first, h);
-      real t = RL(0.0), q = -RL(1.0);
-      int ord = 0;
-      if (work) {
-        const PrimRec r = ld_rec(cf(P.prims) + 16 * (size_t)(first_h + kw));
-        isect_plane<0>(r, Rh.o, Rh, tmin_up, RT_R2I(r.b.w) == Rh.self_gid, t, q);
-        ord = RT_R2I(r.c.w);
-      }
-      // the holders take their pairs' results
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int p = off + k - base;
-        const bool mine = k < cnt && p >= 0 && p < n_act;
-        const int w = mine ? row_lanes[p] : lane;
-        const real tt = __shfl(t, w), qq = __shfl(q, w);
-        const int oo = __shfl(ord, w);
-        if (mine) consider<false>(S.C, tt, qq, oo, first + k);
-      }
-    }
-    if (hold) {
-      S.leaf = 0;
-      if (S.node < 0 && S.node != RT_EMPTY_ROOT) {  // the node we stopped at is a leaf too: next round
-        S.leaf = S.node;
-        S.node = pop_fn(S, W);
-      }
-    }
-  }
-}
-#endif
 // One while-while round: descend until this lane (and the wave) holds a leaf, then test leaves.
 // kInst (two-level instancing): a child RT_INST_FLAG | k enters placement k — the lane's ray R
 // is moved to object space, RT_INST_EXIT is pushed and the object's BVH is traversed; popping
@@ -1297,17 +1225,6 @@ RT_FN void trav_round(const KernelParams& P, RC& R, TravState& S, const Trav& W,
   }
   unsigned long long pf_c1 = RT_PROF_CLK();
   RT_PROF_PADD(PF_NODE_CLK, pf_c1 - pf_c0);
-#if defined(RT_LEAF_PARALLEL) && !defined(RT_HOST_EMU)
-  if constexpr (kLeaf == 1 && !kInst) {
-    leaf_round_parallel(P, R, S, W, [](TravState& T, const Trav& V) -> int {
-      if (T.sp == 0) return RT_EMPTY_ROOT;
-      --T.sp;
-      return V.stack[RT_STACK_ROW(T.sp, V.stride)];
-    });
-    RT_PROF_PADD(PF_LEAF_CLK, RT_PROF_CLK() - pf_c1);
-    return;
-  }
-#endif
   while (S.leaf < 0) {
     RT_PROF_PADD(PF_LEAF_STEPS, 1);
     RT_PROF_PADD(PF_LEAF_LANES, RT_BALLOT_COUNT(true));
