@@ -3,10 +3,13 @@
 // default from the same rt_render_kernel.h), and the 8-bit output epilogue.  The per-lane logic
 // lives in rt_trace.h.
 //
-// rt_render_kernel: a grid of exactly the resident workgroups (occupancy query), 256 lanes each,
-// instantiated per scene class (texture level, media, materials; see render_kernel_of).  Waves
-// start with a static pool of RT_POOL item ids and refill it with one returning atomicAdd on the
-// queue head (ballot the lanes that need work; ids are handed out in lane order); ids are
+// rt_render_kernel: a grid of exactly the resident workgroups (occupancy query), instantiated per
+// scene class (texture level, media, materials, leaf class, instancing; see render_kernel_of).
+// Workgroups: one wave (64 lanes) for the flat kernels; 768 or 1024 lanes for the BVH classes at
+// 3 / 6 or 4 / 8 waves per SIMD, 256 otherwise (rt_render_kernel.h RT_BLOCK_OF; 512-lane twins for
+// deep BVHs).  Waves start with a static pool of item ids and refill it with one returning
+// atomicAdd on one of four queue heads (ballot the lanes that need work; ids are handed out in
+// lane order); ids are
 // pixel-major, so a pool covers a few pixels (coherent primary rays) and its items' int64
 // fixed-point sums are added up per pixel in the wave's LDS slot before one 64-bit atomic per
 // word goes to HBM (commutative: bit-exact for any schedule; rt_render_kernel.h WaveWork).  Each

@@ -304,10 +304,11 @@ struct WaveWork {
 //    from shading per lane (rt_trace.h lane_loop_bvh); the lockstep loop runs every query of a
 //    segment with the whole wave (kept for experiments; images are bit-identical).
 // Register budget: occupancy floor (waves per SIMD), per kernel class and precision — the table
-// below (RT_WAVES_OF): FP32 flat 7 (5 with noise textures), FP32 BVH 6 without media and constant
-// textures, else 5; FP32 flat with constant textures 8; binary64 flat 5 (constant textures, the
-// diffuse materials) / 2, binary64 BVH 4, 3 with media.  Each entry was measured
-// against its neighbours.
+// below (RT_WAVES_OF), each entry measured against its neighbours (DESIGN_HISTORY §1a,
+// §4).  Since round 6 every entry also keeps its class free of VGPR spills (tools/spill_gate.py
+// fails the build otherwise): the binary64 full-material BVH classes, the binary64 instanced
+// full-material class, the FP32 full-material generic-leaf class and the FP32 instanced media-chain
+// classes each run one wave less than their round-5 entries.
 #ifndef RT_WAVES_FLAT
 #define RT_WAVES_FLAT 7
 #endif
