@@ -1407,6 +1407,59 @@ RT_FN void medium_event(const KernelParams& P, int m, uint32_t pix, int sample, 
   medium_draw(P, m, medium_block(P, m, pix, sample, seg), lo, hi, tbest, hit_medium);
 }
 
+// The HemisphereF / SphereF scatter (Ray.hs:187-224): the direction from the redirect mixture
+// (target k by the cumulative probabilities, else the default sampler) and the weight
+// f pdf1 / pdf with pdf = remProb pdf1 + sum_k p_k t_k^2 / |(U_k x V_k) . dir|.  Returns false
+// when a HemisphereF direction is below the surface (pdf1 <= 0: the path ends, Ray.hs:198).
+// kEarly: return there, newdir and Tf untouched (the full-material kernels, whose register
+// allocation needs the short exit); otherwise they are written either way.
+template <bool kMats, bool kEarly>
+RT_FN bool mixture_scatter(const KernelParams& P, const HitInfo& h, const RayCtx& R, const u4& w, const DevMaterial& Mt,
+                           bool hemi, f3 tex, f3& newdir, f3& Tf) {
+  real cr = u01(w.x);
+  int choice = -1;
+  for (int k = 0; k < P.n_targets; ++k) {
+    if (cr < P.targets[k].thresh) {
+      choice = k;
+      break;
+    }
+  }
+  f3 dir;
+  if (choice < 0) {
+    f3 uu = unit_vector(w.y, w.z);
+    dir = hemi ? normalize(h.n + uu) : uu;
+  } else {
+    const DevTarget& Tg = P.targets[choice];
+    f3 lp = ld3(Tg.q) + u01(w.y) * ld3(Tg.u) + u01(w.z) * ld3(Tg.v);
+    dir = normalize(lp - h.p);
+  }
+  real pdf1 = hemi ? dot(dir, h.n) * (RL(1.0) / kPi) : RL(0.25) / kPi;
+  if constexpr (kEarly)
+    if (hemi && pdf1 <= RL(0.0)) return false;
+  real mix = RL(0.0);
+  for (int k = 0; k < P.n_targets; ++k) {
+    // p t^2 / |(u x v) . dir| (Ray.hs:202) with (u x v) . dir = |u x v| (n . dir): the target
+    // test's reciprocal serves both
+    real tt, rinv;
+    if (target_hit(P.targets[k], h.p, dir, tt, rinv)) mix += P.targets[k].prob_icr * (tt * tt * RABS(rinv));
+  }
+  real pdf = P.rem_prob * pdf1 + mix;
+  f3 f = tex;
+  if constexpr (kMats) {
+    if (Mt.kind == 3) {  // lommelSeeliger
+      real mu0 = -dot(R.d, h.n), mu1 = dot(dir, h.n);
+      f = (RL(0.25) * RT_RCP(mu0 + mu1)) * f;
+    } else if (Mt.kind == 9) {  // anisotropic (Henyey-Greenstein)
+      real g = Mt.param, mu = dot(R.d, dir);
+      real base = RL(1.0) + g * g - RL(2.0) * g * mu;
+      f = ((RL(1.0) - g * g) * RT_RCP(base * RT_SQRT(base))) * f;
+    }
+  }
+  Tf = (pdf1 * RT_RCP(pdf)) * f;
+  newdir = dir;
+  return !(hemi && pdf1 <= RL(0.0));
+}
+
 // One rayColor level after the closest hit (Ray.hs:176-224): background on a miss, else the
 // material of the surface / medium hit.  Updates L, T and, when the path continues, the ray
 // (and seg).  Returns true when the path terminates.
@@ -1425,6 +1478,9 @@ RT_FN bool shade_event(const KernelParams& P, cfp prims, uint32_t pix, int sampl
       bg = (RL(1.0) - a) * bg + a * ld3(P.cam.bg1);
     }
     L = L + T * bg;
+#ifndef RT_HOST_EMU
+    Tf = bg;  // (defined, in a register already; the path ends)
+#endif
     return true;
   }
   bool terminate = false;
@@ -1482,111 +1538,62 @@ RT_FN bool shade_event(const KernelParams& P, cfp prims, uint32_t pix, int sampl
   f3 newdir = R.d;
   Tf = tex;
 #endif
-  switch (Mt.kind) {
-    case 0:  // lightSource: emit, Absorb
-      L = L + T * tex;
-      terminate = true;
-      break;
-    case 1:  // pitchBlack
-      terminate = true;
-      break;
-    case 4:  // mirror
-      if constexpr (!kMats) {  // not in this scene (the host compiles these materials in when used)
+  if constexpr (!kMats) {
+    // lightSource / pitchBlack / lambertian only (the Cornell box, the bunny): every hit lane runs
+    // the lambertian scatter, the light and black lanes too, which then end the path (Absorb,
+    // Material.hs:41-47) and never read it.  In a wave the scatter runs whenever any lane is
+    // diffuse, so their lanes cost nothing extra, and the direction and weight come out defined
+    // on every path without a terminating branch of their own
+    if (Mt.kind == 0) L = L + T * tex;  // lightSource: emit
+    terminate = !mixture_scatter<false, false>(P, h, R, w, Mt, true, tex, newdir, Tf) || Mt.kind < 2;
+  } else {
+    switch (Mt.kind) {
+      case 0:  // lightSource: emit, Absorb
+        L = L + T * tex;
         terminate = true;
         break;
-      }
-      Tf = tex;
-      newdir = unit(reflect(h.n, R.d));
-      break;
-    case 5: {  // metal
-      if constexpr (!kMats) {  // not in this scene (the host compiles these materials in when used)
+      case 1:  // pitchBlack
         terminate = true;
         break;
-      }
-      f3 d2 = reflect(h.n, R.d) + Mt.param * unit_vector(w.y, w.z);
-      if (dot(d2, h.n) > RL(0.0)) {
+      case 4:  // mirror
         Tf = tex;
-        newdir = normalize(d2);
-      } else {
-        terminate = true;
-      }
-      break;
-    }
-    case 6: {  // dielectric
-      if constexpr (!kMats) {  // not in this scene (the host compiles these materials in when used)
-        terminate = true;
-        break;
-      }
-      Tf = mk3(RL(1.), RL(1.), RL(1.));
-      real ior = Mt.param;
-      real ratio = h.front ? RT_RCP(ior) : ior;
-      real cos_t = RMIN(RL(1.0), -dot(h.n, R.d));
-      real sin_t = RT_SQRT(RMAX(RL(0.0), RL(1.0) - cos_t * cos_t));
-      real r0 = (RL(1.0) - ratio) * RT_RCP(RL(1.0) + ratio);
-      r0 = r0 * r0;
-      real x1 = RL(1.0) - cos_t, x2 = x1 * x1;
-      real reflectance = r0 + (RL(1.0) - r0) * (x2 * x2 * x1);
-      if (ratio * sin_t > RL(1.0) || u01(w.x) < reflectance) {
         newdir = unit(reflect(h.n, R.d));
-      } else {
-        f3 perp = ratio * (R.d + cos_t * h.n);
-        newdir = unit(perp - RT_SQRT(RABS(RL(1.0) - dot(perp, perp))) * h.n);
-      }
-      break;
-    }
-    case 7:  // transparent
-      if constexpr (!kMats) {  // not in this scene (the host compiles these materials in when used)
-        terminate = true;
         break;
-      }
-      Tf = tex;
-      newdir = R.d;
-      break;
-    default: {  // 2 lambertian, 3 lommelSeeliger (HemisphereF); 8 isotropic, 9 anisotropic (SphereF)
-      const bool hemi = !kMats || Mt.kind == 2 || Mt.kind == 3;
-      real cr = u01(w.x);
-      int choice = -1;
-      for (int k = 0; k < P.n_targets; ++k) {
-        if (cr < P.targets[k].thresh) {
-          choice = k;
-          break;
+      case 5: {  // metal
+        f3 d2 = reflect(h.n, R.d) + Mt.param * unit_vector(w.y, w.z);
+        if (dot(d2, h.n) > RL(0.0)) {
+          Tf = tex;
+          newdir = normalize(d2);
+        } else {
+          terminate = true;
         }
-      }
-      f3 dir;
-      if (choice < 0) {
-        f3 uu = unit_vector(w.y, w.z);
-        dir = hemi ? normalize(h.n + uu) : uu;
-      } else {
-        const DevTarget& Tg = P.targets[choice];
-        f3 lp = ld3(Tg.q) + u01(w.y) * ld3(Tg.u) + u01(w.z) * ld3(Tg.v);
-        dir = normalize(lp - h.p);
-      }
-      real pdf1 = hemi ? dot(dir, h.n) * (RL(1.0) / kPi) : RL(0.25) / kPi;
-      if (hemi && pdf1 <= RL(0.0)) {
-        terminate = true;
         break;
       }
-      real mix = RL(0.0);
-      for (int k = 0; k < P.n_targets; ++k) {
-        // p t^2 / |(u x v) . dir| (Ray.hs:202) with (u x v) . dir = |u x v| (n . dir): the target
-        // test's reciprocal serves both
-        real tt, rinv;
-        if (target_hit(P.targets[k], h.p, dir, tt, rinv)) mix += P.targets[k].prob_icr * (tt * tt * RABS(rinv));
+      case 6: {  // dielectric
+        Tf = mk3(RL(1.), RL(1.), RL(1.));
+        real ior = Mt.param;
+        real ratio = h.front ? RT_RCP(ior) : ior;
+        real cos_t = RMIN(RL(1.0), -dot(h.n, R.d));
+        real sin_t = RT_SQRT(RMAX(RL(0.0), RL(1.0) - cos_t * cos_t));
+        real r0 = (RL(1.0) - ratio) * RT_RCP(RL(1.0) + ratio);
+        r0 = r0 * r0;
+        real x1 = RL(1.0) - cos_t, x2 = x1 * x1;
+        real reflectance = r0 + (RL(1.0) - r0) * (x2 * x2 * x1);
+        if (ratio * sin_t > RL(1.0) || u01(w.x) < reflectance) {
+          newdir = unit(reflect(h.n, R.d));
+        } else {
+          f3 perp = ratio * (R.d + cos_t * h.n);
+          newdir = unit(perp - RT_SQRT(RABS(RL(1.0) - dot(perp, perp))) * h.n);
+        }
+        break;
       }
-      real pdf = P.rem_prob * pdf1 + mix;
-      f3 f = tex;
-      if (!kMats) {
-      } else if (Mt.kind == 3) {
-        real mu0 = -dot(R.d, h.n), mu1 = dot(dir, h.n);
-        f = (RL(0.25) * RT_RCP(mu0 + mu1)) * f;
-      } else if (Mt.kind == 9) {
-        real g = Mt.param, mu = dot(R.d, dir);
-        real base = RL(1.0) + g * g - RL(2.0) * g * mu;
-        f = ((RL(1.0) - g * g) * RT_RCP(base * RT_SQRT(base))) * f;
-      }
-      Tf = (pdf1 * RT_RCP(pdf)) * f;
-      newdir = dir;
-      break;
+      case 7:  // transparent
+        Tf = tex;
+        newdir = R.d;
+        break;
+      default:  // 2 lambertian, 3 lommelSeeliger (HemisphereF); 8 isotropic, 9 anisotropic (SphereF)
+        terminate = !mixture_scatter<true, true>(P, h, R, w, Mt, Mt.kind == 2 || Mt.kind == 3, tex, newdir, Tf);
+        break;
     }
   }
   np = h.p;
@@ -1594,15 +1601,15 @@ RT_FN bool shade_event(const KernelParams& P, cfp prims, uint32_t pix, int sampl
   ngid = h.gid;
   return terminate;
 }
-// One rayColor level (shade_event) and the path's next segment.  The next origin, direction,
-// throughput factor and self id are defined only where the path goes on (no exit of shade_event
-// carries the unchanged ray to a join), and the loop-carried ray and throughput are written
-// unconditionally: a path that ends is restarted by camera_ray (origin, direction, self ids) with
-// a fresh throughput and segment count before anything reads them.  INVARIANT of the lane loops
-// (lane_loop_lockstep, lane_loop_bvh): after shade returns true, R, T and the self ids are
-// indeterminate (the GPU builds leave them unset, the host emulator poisons them with NaN) and
-// nothing may read them before camera_ray.  In the flat binary64 kernel
-// the joins' copies were ~40 v_mov per lane-loop iteration, and selects in their place ~20.
+// One rayColor level (shade_event) and the path's next segment.  The loop-carried ray and
+// throughput are written unconditionally from shade_event's outputs: where the path goes on they
+// are the next segment's; where it ends they are values of no meaning (defined in the GPU builds,
+// NaN-poisoned in the host emulator) that camera_ray replaces (origin, direction, self ids) with a
+// fresh throughput and segment count before anything reads them.  INVARIANT of the lane loops
+// (lane_loop_lockstep, lane_loop_bvh): after shade returns true nothing reads R, T or the self ids
+// before camera_ray (the emulator tests fail otherwise).  Keeping the unchanged ray on the
+// terminating exits instead cost the flat binary64 kernel ~40 copies per lane-loop iteration
+// (round 4).
 template <int kTex, bool kMats, bool kInst = false>
 RT_FN bool shade(const KernelParams& P, cfp prims, uint32_t pix, int sample, int& seg, real tbest, int best,
                  int hit_medium, RayCtx& R, f3& L, f3& T, int best_inst = -1) {
