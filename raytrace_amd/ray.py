@@ -31,13 +31,15 @@ def _seed64(seed) -> int:
 
 
 def raytrace(settings: CameraSettings, world, seed, device: int = 0, stats: dict | None = None,
-             precision: str = "f64", devices=None, row_block: int = 4, encode: str | None = None) -> np.ndarray:
+             precision: str = "f64", devices=None, row_block: int = 4, encode: str | None = None,
+             out: np.ndarray | None = None) -> np.ndarray:
     """Render on the GPU.  Returns (height, width, 3) linear RGB: float64 computed in binary64 as the
     reference does (default), or float32 from the FP32 kernel (precision="f32").  `devices`: a list
     of HIP devices that render the image together from this process (rt_exec device list; rows
     dealt round-robin in blocks of `row_block`); the image is identical to the one-device render.
     `encode` = "srgb" / "sqrt": uint8 codes as writeImage / writeImageSqrt store them, encoded on
-    the device after the gather (Ray.hs:248-260; equal to encode8 of the linear render)."""
+    the device after the gather (Ray.hs:248-260; equal to encode8 of the linear render).  `out`: a
+    caller-held output array to render into (shape and dtype as returned)."""
     L = _lib.load()
     flat = world if isinstance(world, FlatScene) else flatten(world)
     cs = _lib.camera_struct(settings)
@@ -52,7 +54,7 @@ def raytrace(settings: CameraSettings, world, seed, device: int = 0, stats: dict
     rows = _lib.check(L.rt_shard_rows(h, ctypes.byref(ex)))
     if rows != h:
         raise RuntimeError(f"librt_amd.so reports {rows} rows for a {h}-row image")
-    out = np.zeros((h, w, 3), np.uint8 if encode else _lib.dtype_of(precision))
+    out = _out_buffer(out, (h, w, 3), np.uint8 if encode else _lib.dtype_of(precision))
     st = _lib.RtStats()
     _lib.check(L.rt_render(ctypes.byref(cs), ctypes.byref(sc), _seed64(seed), ctypes.byref(ex),
                            out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st)))
@@ -103,6 +105,18 @@ def assemble_shards(tiles, height: int, row_block: int) -> np.ndarray:
         keep = rows < height
         img[rows[keep]] = tiles[r][keep]
     return img
+
+
+def _out_buffer(out, shape, dtype) -> np.ndarray:
+    """The output array: a new one, or the caller's after checking that the library may write the
+    whole frame into it (shape, dtype, C-contiguous, writeable)."""
+    if out is None:
+        return np.zeros(shape, dtype)
+    if not isinstance(out, np.ndarray) or out.shape != tuple(shape) or out.dtype != np.dtype(dtype) \
+            or not out.flags.c_contiguous or not out.flags.writeable:
+        from .errors import RtInvalid
+        raise RtInvalid(f"out must be a writeable C-contiguous {np.dtype(dtype)} array of shape {tuple(shape)}")
+    return out
 
 
 class DeviceScene:
@@ -160,11 +174,13 @@ class MultiDeviceScene:
         self.handle = h
 
     def render(self, settings: CameraSettings, seed, precision: str = "f64", row_block: int = 4,
-               encode: str | None = None, stats: dict | None = None) -> np.ndarray:
+               encode: str | None = None, stats: dict | None = None, out: np.ndarray | None = None) -> np.ndarray:
+        """`out`: a caller-held (h, w, 3) C-contiguous buffer of the output dtype, reused across
+        renders (a fresh array costs its page faults in the device-to-host copy on every call)."""
         cs = _lib.camera_struct(settings)
         ex = _lib.exec_struct(device=self.devices[0], precision=precision, row_block=row_block, encode=encode)
         h, w = image_height(settings), int(settings.cs_imageWidth)
-        out = np.zeros((h, w, 3), np.uint8 if encode else _lib.dtype_of(precision))
+        out = _out_buffer(out, (h, w, 3), np.uint8 if encode else _lib.dtype_of(precision))
         st = _lib.RtStats()
         _lib.check(self._lib.rt_multi_render(self.handle, ctypes.byref(cs), _seed64(seed), ctypes.byref(ex),
                                              out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st)))

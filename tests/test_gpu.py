@@ -455,6 +455,15 @@ def test_multi_device_scene_and_encoded_output(gpu, precision):
     # one entry, rendering an rt_exec shard: the multi-device call with a single device
     single = R.MultiDeviceScene(world, [0])
     np.testing.assert_array_equal(single.render(cs, seed, precision=precision), a)
+    # a caller-held output buffer (poisoned between renders) is overwritten with the same frame
+    buf = np.full(a.shape, np.nan, a.dtype)
+    assert single.render(cs, seed, precision=precision, out=buf) is buf
+    np.testing.assert_array_equal(buf, a)
+    buf[:] = np.nan
+    np.testing.assert_array_equal(single.render(cs, seed, precision=precision, out=buf), a)
+    codes = np.full(a.shape, 7, np.uint8)
+    np.testing.assert_array_equal(R.raytrace(cs, world, seed, precision=precision, encode="srgb", out=codes),
+                                  R.encode8(a, "srgb"))
     single.close()
 
 

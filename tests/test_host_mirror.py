@@ -220,3 +220,21 @@ def test_experiment_knobs_ignored_without_the_switch(emu_mod, monkeypatch):
     monkeypatch.setenv("RT_AMD_EXPERIMENTS", "1")  # switched on, the knobs change the host build
     on = emu_mod.scene_info(world)
     assert on["prefix"] == 0 and on["boxes"] == 0 and on != info
+
+
+def test_caller_output_buffer_is_checked():
+    # raytrace(..., out=) / MultiDeviceScene.render(..., out=): the library writes the whole frame
+    # into the caller's array, so anything it could not fill is refused before any device call
+    from raytrace_amd.errors import RtInvalid
+    from raytrace_amd.ray import _out_buffer
+    buf = np.empty((4, 5, 3), np.float64)
+    assert _out_buffer(buf, (4, 5, 3), np.float64) is buf
+    assert _out_buffer(None, (4, 5, 3), np.uint8).dtype == np.uint8
+    for bad in (np.empty((4, 5, 3), np.float32), np.empty((5, 4, 3)), np.empty((4, 5, 3, 1)),
+                np.empty((4, 10, 3))[:, ::2], [[0.0]]):
+        with pytest.raises(RtInvalid):
+            _out_buffer(bad, (4, 5, 3), np.float64)
+    ro = np.empty((4, 5, 3))
+    ro.flags.writeable = False
+    with pytest.raises(RtInvalid):
+        _out_buffer(ro, (4, 5, 3), np.float64)
