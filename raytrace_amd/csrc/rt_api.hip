@@ -224,7 +224,7 @@ int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_
   KernelParamsT<R> P;
   std::memset(&P, 0, sizeof P);
   if (lone && (s->variant & RT_VAR_BASE) == RT_VAR_FLAT) P.pool_shift = 6;
-  if (const char* e = rt_knob("RT_AMD_POOL_SHIFT")) P.pool_shift = std::max(6, std::min(10, atoi(e)));
+  if (const char* e = rt_knob("RT_AMD_POOL_SHIFT")) P.pool_shift = std::max(4, std::min(10, atoi(e)));
   std::string err;
   int rc = rt_host_make_params(cs, seed, ex, P, err);
   if (rc) return fail(rc, "%s", err.c_str());

@@ -1016,7 +1016,7 @@ template <class R>
 void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_sizes) {
   P.div_width = rt_host_fastdiv((uint32_t)P.cam.width);
   P.div_block = rt_host_fastdiv((uint32_t)P.row_block);
-  if (P.pool_shift < 6) P.pool_shift = __builtin_ctz(RT_POOL);  // (the caller may set 6: 64-id pools)
+  if (P.pool_shift < 4) P.pool_shift = __builtin_ctz(RT_POOL);  // (the caller may set 4-10: 16- to 1024-id pools)
   P.trav_exit_pct = 50;  // the caller sets the scene's policy (HostScene::trav_exit_pct) afterwards
   // Items = (tile pixel, chunk of consecutive samples), claimed in pixel order.  Small chunks
   // keep the 64 lanes of a wave on neighbouring pixels (coherent rays) and make the queue tail
