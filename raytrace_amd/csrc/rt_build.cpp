@@ -215,7 +215,9 @@ void fill_records(const rt_scene* sc, const std::vector<int>& order, const std::
   for (size_t b = 0; b < boxes.size(); ++b) {
     DevBoxT<R> d;
     std::memset(&d, 0, sizeof d);
-    put3(d.c, boxes[b].c);
+    // the slab offsets a_k . c in binary64, rounded once (the kernel's s_k = a_k . o - sc[k], three
+    // FMAs per axis instead of the ray origin relative to the corner and a dot product)
+    for (int k = 0; k < 3; ++k) d.sc[k] = (R)dot(boxes[b].a[k], boxes[b].c);
     put3(d.a0, boxes[b].a[0]);
     put3(d.a1, boxes[b].a[1]);
     put3(d.a2, boxes[b].a[2]);

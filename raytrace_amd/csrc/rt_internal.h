@@ -211,7 +211,7 @@ struct DevFlatSet {
 #define RT_BOX_NO_FACE 31
 template <class R>
 struct DevBoxT {
-  R c[3];          // corner (s = 0 on every axis)
+  R sc[3];         // a_k . c for the corner c (s = 0 on every axis): s_k = a_k . p - sc[k]
   int ord_base;    // key order (flat: slot; prefix: depth-first order) of the faces
   R a0[3];         // axis_0 / L_0: s_0 = a0 . (p - c) in [0, 1] inside
   int ord_code;

@@ -673,7 +673,6 @@ RT_FN bool box_face(const RT_CAS DevBox* B, int f, real q, const RayCtx& R, int&
 template <bool kKeyOnly, bool kInst = false>
 RT_FN void test_box(const RT_CAS DevBox* B, const RayCtx& R, real tmin_up, Closest& C) {
   RT_COUNT(1);
-  const f3 oc = R.o - f3{B->c[0], B->c[1], B->c[2]};
   const f3 ax[3] = {f3{B->a0[0], B->a0[1], B->a0[2]}, f3{B->a1[0], B->a1[1], B->a1[2]},
                     f3{B->a2[0], B->a2[1], B->a2[2]}};
   real lo[3], hi[3];
@@ -705,7 +704,8 @@ RT_FN void test_box(const RT_CAS DevBox* B, const RayCtx& R, real tmin_up, Close
 #else
     const real inv = RT_RCP(dot(ax[k], R.d));
 #endif
-    const real s = dot(ax[k], oc);
+    // s_k = a_k . (o - c) as a_k . o - a_k . c (DevBox::sc, host binary64): one FMA chain
+    const real s = RFMA(ax[k].x, R.o.x, RFMA(ax[k].y, R.o.y, RFMA(ax[k].z, R.o.z, -B->sc[k])));
     const real t0 = -s * inv, t1 = RFMA(-s, inv, inv);  // the s = 0 and s = 1 planes
     // entering through the s = 1 end: t1 - t0 = inv, so t1 < t0 iff inv < 0 (the sign bit; the
     // two differ only when rounding makes t1 == t0, a slab |s| >= 2^52 box widths away)
