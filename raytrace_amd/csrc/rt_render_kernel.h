@@ -121,9 +121,15 @@ struct WaveWork {
         spent(0), pool_slot(-1), slots(slots_),
         hdr(reinterpret_cast<int*>(slots_ + kSlots * AggGeom<kSlots, kPix>::kWords)),
         free_mask(kSlots > 0 ? (1u << kSlots) - 1u : 0u) {
+#if defined(RT_NO_STATIC_POOLS)
+    // (experiment: every pool from the queues, none by wave index)
+    pool_left = 0;
+    offset = 0;
+#else
     // every wave starts with a static pool (its wave index x pool): at launch all resident
     // waves would otherwise queue up on the counter at once (~80 us at ~88 returning atomics per us)
     pool_slot = open_pool(pool_base, min(pool, P.n_items - pool_base));
+#endif
   }
 
   // a slot for the pool of ids [b0, b0 + cnt) (wave-uniform), or -1: commit its items directly.
@@ -246,6 +252,8 @@ struct WaveWork {
   // kp().agg_small, set by the host for tiles below 2^24 pixels); elsewhere the word is the plain tile
   // pixel, whose bits 24-30 may be set (tiles up to 2^31 pixels), and commit must not decode it
   __device__ __forceinline__ bool aggregating() const { return kSlots > 0 && (kp().agg_big | kp().agg_small) != 0; }
+  // an item's plain tile pixel (its slot code cleared; rt_trace.h steal_sample)
+  __device__ __forceinline__ int untag(int tpk) const { return aggregating() ? (tpk & 0xffffff) : tpk; }
   __device__ __forceinline__ int tag(int tp, int slot) const {
     if (slot < 0) return tp;
     return tp | ((slot + 1) << 24);

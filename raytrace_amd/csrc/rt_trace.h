@@ -1681,6 +1681,46 @@ RT_FN bool open_item(const KernelParams& P, int item, ItemCtx& I) {
   return I.sample < I.s_end;
 }
 
+// Sample stealing once the queue is drained (flat lane loop; RT_TAIL_STEAL).  A lane that finds no
+// item left takes the last pending sample of a lane of its wave that still holds two or more (the
+// one in flight and at least one more): the victim's item ends one sample earlier, the thief
+// renders that sample as an item of its own — same pixel, same sample index, so the same Philox
+// draws — and commits it directly (`tp_plain`: the tile pixel without the victim's aggregation
+// slot code, whose open-id count belongs to the victim's commit).  Integer sums commute: the image
+// is bit-identical.  Without it the frame ends on the waves whose lanes still hold up to three
+// samples each (a lane's item of the queue's tail) while their other lanes idle.  Wave-uniform
+// call; one pair per loop step, scalar (readlane) moves.
+#ifndef RT_TAIL_STEAL
+#define RT_TAIL_STEAL 1
+#endif
+#if RT_TAIL_STEAL && !defined(RT_HOST_EMU)
+RT_FN bool steal_sample(bool thief, ItemCtx& I, int tp_plain) {
+  unsigned long long tm = __ballot(thief);
+  unsigned long long vm = __ballot(!thief && I.tp != -1 && I.s_end - I.sample >= 2);
+  const int lane = (int)__lane_id();
+  bool got = false;
+  while (tm != 0ull && vm != 0ull) {
+    const int t = __ffsll(tm) - 1, v = __ffsll(vm) - 1;
+    tm &= tm - 1ull;
+    vm &= vm - 1ull;
+    const int s_end = __builtin_amdgcn_readlane(I.s_end, v);
+    const int tp = __builtin_amdgcn_readlane(tp_plain, v);
+    const uint32_t pix = (uint32_t)__builtin_amdgcn_readlane((int)I.pix, v);
+    const uint32_t pxgy = (uint32_t)__builtin_amdgcn_readlane((int)I.pxgy, v);
+    if (lane == t) {
+      I.tp = tp;
+      I.sample = s_end - 1;
+      I.s_end = s_end;
+      I.pix = pix;
+      I.pxgy = pxgy;
+      got = true;
+    }
+    if (lane == v) I.s_end = s_end - 1;
+  }
+  return got;
+}
+#endif
+
 // The lockstep persistent lane loop.  `work.grab(need, slot)` is wave-collective: it
 // returns a fresh item for lanes with need == true (and its aggregation slot); `work.commit(c,
 // tile_pixel, acc, bad)`, also wave-collective, adds the finished items' sums of lanes with
@@ -1718,13 +1758,24 @@ RT_FN int lane_loop_lockstep(const KernelParams& P0, Work& work, const Trav& TW,
     work.commit(need && I.tp != -1, I.tp, acc, bad);
     int aslot;
     const int got = work.grab(need, aslot);
+#if RT_TAIL_STEAL && !defined(RT_HOST_EMU)
+    bool stolen = false;
+    if constexpr (kFlat) {
+      const bool thief = need && got >= P.n_items;
+      if (RT_ANY(thief)) stolen = steal_sample(thief, I, work.untag(I.tp));
+    }
+#else
+    const bool stolen = false;
+#endif
     if (need) {
-      if (got >= P.n_items) break;
+      if (got >= P.n_items && !stolen) break;
       acc_clear(acc);
       bad = false;
-      const bool ok = open_item<kFlat>(P, got, I);
-      I.tp = work.tag(I.tp, aslot);
-      if (!ok) continue;
+      if (!stolen) {
+        const bool ok = open_item<kFlat>(P, got, I);
+        I.tp = work.tag(I.tp, aslot);
+        if (!ok) continue;
+      }
     }
     RT_PROF_MARK(PF_FRONT);
     RT_PROF_ADD(PF_CAM_LANES, RT_BALLOT_COUNT(!alive));
