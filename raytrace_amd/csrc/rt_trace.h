@@ -1693,7 +1693,10 @@ RT_FN bool open_item(const KernelParams& P, int item, ItemCtx& I) {
 #ifndef RT_TAIL_STEAL
 #define RT_TAIL_STEAL 1
 #endif
-#if RT_TAIL_STEAL && !defined(RT_HOST_EMU)
+#ifndef RT_TAIL_STEAL_BVH  // (the same in the decoupled BVH lane loop)
+#define RT_TAIL_STEAL_BVH 1
+#endif
+#if (RT_TAIL_STEAL || RT_TAIL_STEAL_BVH) && !defined(RT_HOST_EMU)
 RT_FN bool steal_sample(bool thief, ItemCtx& I, int tp_plain) {
   unsigned long long tm = __ballot(thief);
   unsigned long long vm = __ballot(!thief && I.tp != -1 && I.s_end - I.sample >= 2);
@@ -1940,12 +1943,25 @@ RT_FN int lane_loop_bvh(const KernelParams& P0, Work& work, const Trav& TW, cons
     work.commit(need && I.tp != -1, I.tp, acc, bad);
     int aslot;
     const int got = work.grab(need, aslot);
+#if RT_TAIL_STEAL_BVH && !defined(RT_HOST_EMU)
+    bool stolen = false;
+    {
+      const bool thief = need && got >= P.n_items;
+      if (RT_ANY(thief)) stolen = steal_sample(thief, I, work.untag(I.tp));
+    }
+#else
+    const bool stolen = false;
+#endif
     if (need) {
-      if (got >= P.n_items) break;
+      if (got >= P.n_items && !stolen) break;
       acc_clear(acc);
       bad = false;
-      state = open_item<false>(P, got, I) ? ST_NEED_SAMPLE : ST_NEED_ITEM;
-      I.tp = work.tag(I.tp, aslot);
+      if (stolen) {
+        state = ST_NEED_SAMPLE;
+      } else {
+        state = open_item<false>(P, got, I) ? ST_NEED_SAMPLE : ST_NEED_ITEM;
+        I.tp = work.tag(I.tp, aslot);
+      }
     }
     if (state == ST_NEED_SAMPLE) {
       camera_ray(P, I.pix, I.sample, ~0u, R);
