@@ -321,6 +321,25 @@ def test_item_chunk_does_not_change_the_image(knobs, gpu, monkeypatch, name, pre
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("name", ["cornell", "bunny_cornell"])
+def test_tail_stealing_is_exact(knobs, gpu, monkeypatch, name, precision):
+    """64 pixels x 600 samples: the queue drains at once and most samples are rendered by lanes
+    that took them from another lane's item (rt_trace.h steal_sample, both lane loops).  One-sample
+    items leave nothing to take; 16- and 64-sample items are split across the wave.  The stolen
+    samples keep their pixel and sample index (the same Philox draws) and integer sums commute, so
+    the images are bit-identical."""
+    fn = {"cornell": scenes.cornell_box, "bunny_cornell": scenes.bunny_cornell}[name]
+    cs, world, seed = fn(width=8, spp=600)
+    imgs = []
+    for c in ("1", "16", "64"):
+        monkeypatch.setenv("RT_AMD_CHUNK", c)
+        imgs.append(R.raytrace(cs, world, seed, precision=precision))
+    for img in imgs[1:]:
+        assert np.array_equal(img, imgs[0], equal_nan=True)
+    assert np.isfinite(imgs[0]).all() and imgs[0].mean() > 0
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("name", ["cornell", "bunny_cornell", "pawn_fog"])
 def test_commit_aggregation_is_exact(knobs, gpu, monkeypatch, name, precision):
     """Items summed per pixel in the waves' LDS slots before the commit atomics (rt_render_kernel.h
