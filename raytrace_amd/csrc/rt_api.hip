@@ -254,7 +254,7 @@ int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_
   P.lds_nodes = A.lds_nodes;
   P.n_prims = s->n_prims;
   rt_host_plan_work(P, (long long)A.resident_blocks * rt_render_block((const KernelParamsT<R>*)nullptr, s->variant),
-                    (s->variant & RT_VAR_BASE) == RT_VAR_FLAT);
+                    (s->variant & RT_VAR_BASE) == RT_VAR_FLAT, lone);
   P.trav_exit_pct = sizeof(R) == 8 ? s->trav_exit_pct64 : s->trav_exit_pct;
   P.out_frame_rows = frame_rows;
   HIP_TRY(hipSetDevice(s->device));

@@ -1015,7 +1015,7 @@ FastDiv rt_host_fastdiv(uint32_t d) {
 }
 
 template <class R>
-void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_sizes) {
+void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_sizes, bool lone) {
   P.div_width = rt_host_fastdiv((uint32_t)P.cam.width);
   P.div_block = rt_host_fastdiv((uint32_t)P.row_block);
   if (P.pool_shift < 4) P.pool_shift = __builtin_ctz(RT_POOL);  // (the caller may set 4-10: 16- to 1024-id pools)
@@ -1044,13 +1044,17 @@ void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_s
   }
   // Big items for the bulk of the samples, small ones for the tail: the last T samples of every
   // pixel go in `chunk`-sample items, T such that the tail alone still gives every resident lane
-  // RT_TAIL_ITEMS_* items (the queue's end stays as short as with small items only), and the
-  // first spp - T in as few items of at most RT_BIG_CHUNK_MAX samples as cover them exactly
-  // (at most 48: Cornell binary64 at 1 GPU would take 16 items per pixel instead of 23 and as many
-  // fewer commit atomics, but runs 1.5 % slower (6.19 vs 6.10 ms, profiles/r3/iso), so 16).
-  int big = RT_BIG_CHUNK_MAX, n_big = 0;
+  // `tail_items` items, and the first spp - T in as few items of at most `big` samples as cover
+  // them exactly.  Two policies since the tail sample stealing (round 6, profiles/r6/sweeps/big):
+  // * renders whose frames overlap (rt_render_async: the bench line) take up to 64-sample big items
+  //   and 8 tail items per lane — fewer item openings and commits, and the next frame fills the
+  //   longer end: Cornell binary64 4.858 -> 4.761 ms, FP32 2.950 -> 2.800, README binary64 0.407
+  //   -> 0.392, the 8-GPU share unchanged (its tail covers every sample);
+  // * a synchronous call's one launch ends on its last big items, so it keeps 16-sample items and
+  //   16 / 32 tail items (one Cornell call 5.25 ms against 5.49 with 48-sample items).
+  int big = lone ? RT_BIG_CHUNK_MAX : RT_BIG_CHUNK_MAX_ASYNC, n_big = 0;
   if (const char* env = rt_knob("RT_AMD_BIG_CHUNK")) big = std::max(1, std::atoi(env));
-  int tail_items = sizeof(R) == 8 ? RT_TAIL_ITEMS_F64 : RT_TAIL_ITEMS_F32;
+  int tail_items = !lone ? RT_TAIL_ITEMS_ASYNC : sizeof(R) == 8 ? RT_TAIL_ITEMS_F64 : RT_TAIL_ITEMS_F32;
   if (const char* env = rt_knob("RT_AMD_TAIL_ITEMS")) tail_items = std::atoi(env);
   if (two_sizes && chunk < big && tail_items > 0 && resident_lanes > 0 && tile_pixels > 0) {
     long long t = ((long long)tail_items * chunk * resident_lanes + tile_pixels - 1) / tile_pixels;
@@ -1095,8 +1099,8 @@ template int rt_host_make_params<float>(const rt_camera_settings*, uint64_t, con
                                         std::string&);
 template int rt_host_make_params<double>(const rt_camera_settings*, uint64_t, const rt_exec*, KernelParamsT<double>&,
                                          std::string&);
-template void rt_host_plan_work<float>(KernelParamsT<float>&, long long, bool);
-template void rt_host_plan_work<double>(KernelParamsT<double>&, long long, bool);
+template void rt_host_plan_work<float>(KernelParamsT<float>&, long long, bool, bool);
+template void rt_host_plan_work<double>(KernelParamsT<double>&, long long, bool, bool);
 
 // The 8-bit code thresholds of writeImage / writeImageSqrt's quantisation (rt_encode8_table.h,
 // generated with the transfer evaluated exactly; raytrace_amd.ray.encode8 reads the same table).

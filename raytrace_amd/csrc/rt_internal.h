@@ -65,7 +65,10 @@
 #define RT_AGG_PIX_BVH 5  // n >= 32 (the BVH kernels' LDS is node staging too)
 #endif
 #ifndef RT_BIG_CHUNK_MAX
-#define RT_BIG_CHUNK_MAX 16  // samples per big work item at most (rt_build.cpp rt_host_plan_work; 38-48: Cornell f64 +1.5 %)
+#define RT_BIG_CHUNK_MAX 16  // samples per big work item at most, synchronous calls (rt_build.cpp rt_host_plan_work)
+#endif
+#ifndef RT_BIG_CHUNK_MAX_ASYNC
+#define RT_BIG_CHUNK_MAX_ASYNC 64  // ... renders whose frames overlap (rt_render_async)
 #endif
 // small items per resident lane kept for the queue tail (rt_build.cpp rt_host_plan_work; 0: one
 // item size).  Cornell 600x600x200, same box (profiles/r2/items/): binary64 6.77 -> 6.63 ms at
@@ -75,6 +78,9 @@
 #endif
 #ifndef RT_TAIL_ITEMS_F32
 #define RT_TAIL_ITEMS_F32 32
+#endif
+#ifndef RT_TAIL_ITEMS_ASYNC  // (both precisions, renders whose frames overlap)
+#define RT_TAIL_ITEMS_ASYNC 8
 #endif
 #define RT_LEAF_SHIFT 6       // leaf encoding ~(first << 6 | count - 1), count <= 64
 #define RT_FLAT_MAX 32        // a set of at most this many leaves is one flat leaf (no traversal)
@@ -407,7 +413,7 @@ int rt_host_make_params(const rt_camera_settings* cs, uint64_t seed, const rt_ex
                         std::string& err);
 // work decomposition (rt_build.cpp): chunk so that items >= ~8 x resident lanes
 template <class R>
-void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_sizes);  // two_sizes: flat kernel
+void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_sizes, bool lone = false);  // two_sizes: flat kernel
 FastDiv rt_host_fastdiv(uint32_t d);
 // the 8-bit code thresholds of the output epilogue (rt_build.cpp): thr[k] = the smallest binary64
 // x in [0, 1] whose code min(255, floor(256 transfer(x))) is >= k (k = 1..255; thr[0] = 0)
