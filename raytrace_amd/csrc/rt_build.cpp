@@ -1018,7 +1018,8 @@ template <class R>
 void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_sizes, bool lone) {
   P.div_width = rt_host_fastdiv((uint32_t)P.cam.width);
   P.div_block = rt_host_fastdiv((uint32_t)P.row_block);
-  if (P.pool_shift < 4) P.pool_shift = __builtin_ctz(RT_POOL);  // (the caller may set 4-10: 16- to 1024-id pools)
+  const bool pool_given = P.pool_shift >= 4;  // (the caller may set 4-10: 16- to 1024-id pools)
+  if (!pool_given) P.pool_shift = __builtin_ctz(RT_POOL);
   P.trav_exit_pct = 50;  // the caller sets the scene's policy (HostScene::trav_exit_pct) afterwards
   // Items = (tile pixel, chunk of consecutive samples), claimed in pixel order.  Small chunks
   // keep the 64 lanes of a wave on neighbouring pixels (coherent rays) and make the queue tail
@@ -1081,6 +1082,10 @@ void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_s
   P.n_big_chunks = n_big;
   P.big_items = (int)((long long)n_big * tile_pixels);
   P.small_start = n_big * big;
+  // long big items (>= 32 samples): 64-id pools, one item per lane, so the waves' last pools are
+  // even (Cornell binary64 4.760 -> 4.730 ms, FP32 2.803 -> 2.782); shorter ones keep RT_POOL ids
+  // per refill (README's 17-sample items: 0.392 -> 0.402 with 64)
+  if (!pool_given && !lone && n_big > 0 && big >= 32) P.pool_shift = 6;
   P.div_big = rt_host_fastdiv((uint32_t)std::max(1, n_big));
   P.div_small = rt_host_fastdiv((uint32_t)std::max(1, P.n_chunks));
   P.n_items = (int)items;
