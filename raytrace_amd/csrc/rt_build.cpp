@@ -1063,9 +1063,21 @@ void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_s
     const long long tail = ((t + chunk - 1) / chunk) * chunk;  // tail samples, a multiple of chunk
     if (tail < spp) {
       const long long bulk = spp - tail;
-      n_big = (int)((bulk + big - 1) / big);
-      big = (int)((bulk + n_big - 1) / n_big);  // <= the maximum; n_big items cover the bulk
-      big = std::min(big, spp / n_big);          // the small items cover [n_big big, spp)
+      auto split = [&](int cap) {
+        n_big = (int)((bulk + cap - 1) / cap);
+        big = (int)((bulk + n_big - 1) / n_big);  // <= cap; n_big items cover the bulk
+        big = std::min(big, spp / n_big);          // the small items cover [n_big big, spp)
+      };
+      split(big);
+      // the waves' first pools are static (rt_render_kernel.h WaveWork): a lane's share of its
+      // first pool's big items must stay below the mean work per lane, or the lanes of the first
+      // waves end the frame alone (README with 26-sample items from 6 tail items: 0.39 -> 0.51 ms)
+      const double per_lane = (double)spp * (double)tile_pixels / (double)resident_lanes;
+      for (int pass = 0; pass < 2 && !lone; ++pass) {  // (the pool follows the item size: below)
+        const int pool_items = (pool_given ? 1 << P.pool_shift : big >= 32 ? 64 : RT_POOL) / 64;
+        const int cap = (int)(0.9 * per_lane / pool_items);
+        if (cap >= 1 && big > cap) split(cap);
+      }
       if (big <= chunk) n_big = 0;
     }
   }
