@@ -308,8 +308,7 @@ def main():
     ap.add_argument("--no-f32", action="store_true", help="skip the FP32 fast-path record after an f64 line")
     ap.add_argument("--streams", type=int, default=0, choices=[0, 1, 2, 3, 4],
                     help="frames alternate between this many HIP streams (2: frame i+1 fills the CUs that "
-                         "frame i's last long paths leave idle); 0 = auto: 2 for flat scenes, 1 for BVH "
-                         "scenes (two LDS-staging BVH launches interfere: bunny 20.7 -> 22.4 ms per frame)")
+                         "frame i's last long paths leave idle); 0 = auto: 2")
     ap.add_argument("--warmup-s", type=float, default=2.0,
                     help="after the W warm-up frames, keep warming up until the warm-up has rendered this "
                          "many seconds (the per-frame time settles after a few hundred ms); 0: exactly W")
@@ -381,7 +380,10 @@ def main():
     scene = DeviceScene(world, device=local_rank)
     rows = shard_rows(h, n_sh, args.row_block)
     if args.streams == 0:
-        args.streams = 2 if scene.stats()["bvh_nodes"] == 0 else 1
+        # two streams for every scene since round 6: with the tail stealing and 1024-lane BVH
+        # workgroups, two overlapped BVH launches no longer interfere (bunny's 8-GPU share 18.84 ->
+        # 18.00 ms, demo1's 7.90 -> 7.53, pawn+fog's 52.39 -> 51.83; profiles/r6/sweeps/streams)
+        args.streams = 2
 
     def measure(precision):
         """Warm up, then time exactly args.steps frames in `precision`; returns the rank's timings."""
