@@ -74,7 +74,8 @@ static_assert((RT_QUEUES & (RT_QUEUES - 1)) == 0 && RT_QUEUES <= 8, "RT_QUEUES: 
 // sums: the image is bit-identical either way.
 // (keeping the item's pixel offset within the slot in its code, resolved at the item's start
 // instead of one LDS read at its commit, measured no faster: Cornell f64 5.77 vs 5.74 ms)
-static_assert(RT_AGG_SLOTS_FLAT < 255 && RT_AGG_SLOTS_BVH < 255, "slot + 1 must fit the 8 bits of rt_trace.h ItemCtx::tp");
+static_assert(RT_AGG_SLOTS_FLAT < 255 && RT_AGG_SLOTS_FLAT_F64 < 255 && RT_AGG_SLOTS_BVH < 255,
+              "slot + 1 must fit the 8 bits of rt_trace.h ItemCtx::tp");
 
 // LDS of the aggregation slots per wave: kSlots x kPix x RT_ACC_WORDS words + 2 kSlots header ints
 template <int kSlots, int kPix>
@@ -442,8 +443,10 @@ struct WaveWork {
 #define RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst, kLeaf) \
   ((kVar) == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH_OF(RT_WAVES_OF(kVar, kTex, kMedia, kMats, kInst, kLeaf)))
 // commit-aggregation slots per wave and pixels per slot of a kernel class (rt_internal.h)
-#define RT_AGG_SLOTS_OF(kVar) ((kVar) == RT_VAR_FLAT ? RT_AGG_SLOTS_FLAT : RT_AGG_SLOTS_BVH)
-#define RT_AGG_PIX_OF(kVar) ((kVar) == RT_VAR_FLAT ? RT_AGG_PIX_FLAT : RT_AGG_PIX_BVH)
+#define RT_AGG_SLOTS_FLAT_R (RT_F64 ? RT_AGG_SLOTS_FLAT_F64 : RT_AGG_SLOTS_FLAT)
+#define RT_AGG_PIX_FLAT_R (RT_F64 ? RT_AGG_PIX_FLAT_F64 : RT_AGG_PIX_FLAT)
+#define RT_AGG_SLOTS_OF(kVar) ((kVar) == RT_VAR_FLAT ? RT_AGG_SLOTS_FLAT_R : RT_AGG_SLOTS_BVH)
+#define RT_AGG_PIX_OF(kVar) ((kVar) == RT_VAR_FLAT ? RT_AGG_PIX_FLAT_R : RT_AGG_PIX_BVH)
 // kMedia: 0 none; 1 the media queries chained in the traversal loop; 2 the media events in the
 // shading phase (RT_VAR_MEDIA_LATE; rt_trace.h media_events_late)
 // kNarrow: the 1024-lane class at 512 lanes, for a scene whose stacks do not fit one 1024-lane
@@ -608,7 +611,7 @@ static bool acc_in_lds(int variant) {
 static size_t render_fixed_lds(int variant) {
   const bool flat = (variant & RT_VAR_BASE) == RT_VAR_FLAT;
   const size_t acc = acc_in_lds(variant) ? (size_t)RT_ACC_WORDS(real) * 8 * render_block(variant) : 0;
-  const size_t agg = (size_t)(flat ? AggGeom<RT_AGG_SLOTS_FLAT, RT_AGG_PIX_FLAT>::kWaveBytes
+  const size_t agg = (size_t)(flat ? AggGeom<RT_AGG_SLOTS_FLAT_R, RT_AGG_PIX_FLAT_R>::kWaveBytes
                                    : AggGeom<RT_AGG_SLOTS_BVH, RT_AGG_PIX_BVH>::kWaveBytes) *
                      (render_block(variant) / 64);
   return acc + agg;
