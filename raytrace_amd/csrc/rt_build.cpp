@@ -1103,7 +1103,9 @@ void rt_host_plan_work(KernelParamsT<R>& P, long long resident_lanes, bool two_s
   P.n_items = (int)items;
   // commit aggregation: a phase qualifies when a pool of RT_POOL consecutive ids spans at most a
   // slot's pixels (rt_render_kernel.h WaveWork); env RT_AMD_AGG=0 turns it off (A/B, same LDS)
-  const int slot_pix = !two_sizes ? RT_AGG_PIX_BVH : sizeof(R) == 8 ? RT_AGG_PIX_FLAT_F64 : RT_AGG_PIX_FLAT;
+  const int slot_pix = !two_sizes                          ? RT_AGG_PIX_BVH
+                       : sizeof(R) == 8 || P.n_media == 0 ? RT_AGG_PIX_FLAT_F64  // (rt_render_kernel.h RT_AGG_WIDE_OF)
+                                                          : RT_AGG_PIX_FLAT;
   const int pool = 1 << P.pool_shift;
   auto spans = [&](int n) { return n > 0 && (pool - 1 + n - 1) / n + 1 <= slot_pix; };
   bool agg = tile_pixels < (1ll << 24);  // the item's aggregation code shares its tile-pixel word

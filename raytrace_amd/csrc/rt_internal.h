@@ -58,10 +58,11 @@
 #ifndef RT_AGG_PIX_FLAT
 #define RT_AGG_PIX_FLAT 17  // n >= 8
 #endif
-// binary64 flat kernels: 7 slots of 22 pixels (7.4 KB of LDS per wave, 20 waves per CU), so that
-// the overlapped-frame plan's ~60-sample big items (3 per pixel, 64-id pools: a 22-pixel span)
-// aggregate too: Cornell 4.728 -> 4.696 ms (profiles/r6/sweeps/agg).  The FP32 kernels keep
-// 8 x 17: their flat media class spills 12 VGPRs with any other geometry
+// the wide flat slots, binary64 flat kernels and FP32 flat kernels without media: 7 slots of 22
+// pixels (binary64: 7.4 KB of LDS per wave, 20 waves per CU), so that the overlapped-frame plan's
+// ~60-sample big items (3 per pixel, 64-id pools: a 22-pixel span) aggregate too: Cornell
+// 4.728 -> 4.696 ms (profiles/r6/sweeps/agg).  The FP32 flat media classes keep 8 x 17: they
+// spill 12 VGPRs with any other geometry
 #ifndef RT_AGG_SLOTS_FLAT_F64
 #define RT_AGG_SLOTS_FLAT_F64 7
 #endif

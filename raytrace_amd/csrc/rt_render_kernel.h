@@ -443,10 +443,13 @@ struct WaveWork {
 #define RT_BLOCK_OF(kVar, kTex, kMedia, kMats, kInst, kLeaf) \
   ((kVar) == RT_VAR_FLAT ? RT_BLOCK : RT_BLOCK_BVH_OF(RT_WAVES_OF(kVar, kTex, kMedia, kMats, kInst, kLeaf)))
 // commit-aggregation slots per wave and pixels per slot of a kernel class (rt_internal.h)
-#define RT_AGG_SLOTS_FLAT_R (RT_F64 ? RT_AGG_SLOTS_FLAT_F64 : RT_AGG_SLOTS_FLAT)
-#define RT_AGG_PIX_FLAT_R (RT_F64 ? RT_AGG_PIX_FLAT_F64 : RT_AGG_PIX_FLAT)
-#define RT_AGG_SLOTS_OF(kVar) ((kVar) == RT_VAR_FLAT ? RT_AGG_SLOTS_FLAT_R : RT_AGG_SLOTS_BVH)
-#define RT_AGG_PIX_OF(kVar) ((kVar) == RT_VAR_FLAT ? RT_AGG_PIX_FLAT_R : RT_AGG_PIX_BVH)
+// (the wide slots: every binary64 flat class, and the FP32 flat classes without media —
+// rt_internal.h RT_AGG_*_FLAT_F64; rt_build.cpp rt_host_plan_work mirrors the choice)
+#define RT_AGG_WIDE_OF(kMedia) (RT_F64 || (kMedia) == 0)
+#define RT_AGG_SLOTS_FLAT_R(kMedia) (RT_AGG_WIDE_OF(kMedia) ? RT_AGG_SLOTS_FLAT_F64 : RT_AGG_SLOTS_FLAT)
+#define RT_AGG_PIX_FLAT_R(kMedia) (RT_AGG_WIDE_OF(kMedia) ? RT_AGG_PIX_FLAT_F64 : RT_AGG_PIX_FLAT)
+#define RT_AGG_SLOTS_OF(kVar, kMedia) ((kVar) == RT_VAR_FLAT ? RT_AGG_SLOTS_FLAT_R(kMedia) : RT_AGG_SLOTS_BVH)
+#define RT_AGG_PIX_OF(kVar, kMedia) ((kVar) == RT_VAR_FLAT ? RT_AGG_PIX_FLAT_R(kMedia) : RT_AGG_PIX_BVH)
 // kMedia: 0 none; 1 the media queries chained in the traversal loop; 2 the media events in the
 // shading phase (RT_VAR_MEDIA_LATE; rt_trace.h media_events_late)
 // kNarrow: the 1024-lane class at 512 lanes, for a scene whose stacks do not fit one 1024-lane
@@ -462,7 +465,7 @@ void rt_render_kernel(KernelParams P) {
 #if defined(RT_WAVE_STAMPS)
   const unsigned long long t_start = wall_clock64();
 #endif
-  constexpr int kSlots = RT_AGG_SLOTS_OF(kVar), kPix = RT_AGG_PIX_OF(kVar);
+  constexpr int kSlots = RT_AGG_SLOTS_OF(kVar, kMedia), kPix = RT_AGG_PIX_OF(kVar, kMedia);
   // (the launch bound; a deep BVH's render may launch fewer lanes: host render_block)
 #if defined(RT_BLOCK_RUNTIME)  // (experiment: the stack stride from blockDim; profiles/r5/bigwg, r6/nondet)
   const int block = (int)blockDim.x;
@@ -611,8 +614,10 @@ static bool acc_in_lds(int variant) {
 static size_t render_fixed_lds(int variant) {
   const bool flat = (variant & RT_VAR_BASE) == RT_VAR_FLAT;
   const size_t acc = acc_in_lds(variant) ? (size_t)RT_ACC_WORDS(real) * 8 * render_block(variant) : 0;
-  const size_t agg = (size_t)(flat ? AggGeom<RT_AGG_SLOTS_FLAT_R, RT_AGG_PIX_FLAT_R>::kWaveBytes
-                                   : AggGeom<RT_AGG_SLOTS_BVH, RT_AGG_PIX_BVH>::kWaveBytes) *
+  const bool wide = RT_F64 || (variant & RT_VAR_MEDIA) == 0;
+  const size_t agg = (size_t)(!flat ? AggGeom<RT_AGG_SLOTS_BVH, RT_AGG_PIX_BVH>::kWaveBytes
+                              : wide ? AggGeom<RT_AGG_SLOTS_FLAT_F64, RT_AGG_PIX_FLAT_F64>::kWaveBytes
+                                     : AggGeom<RT_AGG_SLOTS_FLAT, RT_AGG_PIX_FLAT>::kWaveBytes) *
                      (render_block(variant) / 64);
   return acc + agg;
 }
