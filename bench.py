@@ -306,6 +306,10 @@ def main():
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"],
                     help="the kernel precision of the line's value (f64: the reference's binary64)")
     ap.add_argument("--no-f32", action="store_true", help="skip the FP32 fast-path record after an f64 line")
+    ap.add_argument("--plan", default="auto", choices=["auto", "overlapped", "solo"],
+                    help="work plan of each render (rt_exec RT_EXEC_SOLO): auto = solo with one stream, "
+                         "overlapped otherwise; tools/pmc_run.sh counts one-stream launches of the "
+                         "overlapped plan, the bench line's")
     ap.add_argument("--streams", type=int, default=0, choices=[0, 1, 2, 3, 4],
                     help="frames alternate between this many HIP streams (2: frame i+1 fills the CUs that "
                          "frame i's last long paths leave idle); 0 = auto: 2")
@@ -422,8 +426,10 @@ def main():
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
+            # one stream: frames do not overlap, so each is planned as a lone render (RT_EXEC_SOLO)
+            solo = args.plan == "solo" or (args.plan == "auto" and len(streams) == 1)
             scene.render_async(cs, seed, tile.data_ptr(), stream.cuda_stream, n_shards=n_sh, shard=sh,
-                               row_block=args.row_block, precision=precision)
+                               row_block=args.row_block, precision=precision, solo=solo)
             if timed:
                 e1.record(stream)
                 ev.append((e0, e1))

@@ -197,6 +197,10 @@ typedef struct rt_camera_settings {
    the linear render on the host. */
 #define RT_EXEC_ENCODE8_SRGB 2
 #define RT_EXEC_ENCODE8_SQRT 4
+/* rt_render_async only: this render does not overlap another on the device (one stream, or the
+   caller waits for it), so its work is planned for a short end, as rt_render's: 16-sample big
+   items instead of up to 64 (rt_build.cpp rt_host_plan_work).  Images are identical either way. */
+#define RT_EXEC_SOLO 8
 
 #define RT_MAX_DEVICES 64
 
@@ -279,7 +283,8 @@ int rt_scene_stats(const rt_device_scene* s, rt_stats* stats);
 /* Enqueue one render on `hip_stream` (a hipStream_t, or NULL for the default stream) of the
  * scene's device.  d_out_rgb: device buffer of rt_shard_rows(h, ex) * image_width * 3 doubles
  * (floats with RT_EXEC_F32).  ex->n_devices must be 0.  Asynchronous; the scene must outlive
- * the work. */
+ * the work.  Renders are planned for frames that overlap on two or more streams (the next frame
+ * fills the end of this one); RT_EXEC_SOLO plans a render that runs alone. */
 int rt_render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex,
                     void* d_out_rgb, void* hip_stream);
 

@@ -57,6 +57,7 @@ class RtScene(ctypes.Structure):
 RT_EXEC_F32 = 1  # rt_exec.flags: FP32 kernel, float output (default: binary64, double output)
 RT_EXEC_ENCODE8_SRGB = 2  # rt_render output: uint8 codes of writeImage (sRGB)
 RT_EXEC_ENCODE8_SQRT = 4  # rt_render output: uint8 codes of writeImageSqrt
+RT_EXEC_SOLO = 8  # rt_render_async: the render runs alone (planned for a short end, as rt_render's)
 ENCODINGS = {None: 0, "srgb": RT_EXEC_ENCODE8_SRGB, "sqrt": RT_EXEC_ENCODE8_SQRT}
 ABI_VERSION = 6
 PRECISIONS = {"f64": np.float64, "f32": np.float32}
@@ -186,15 +187,17 @@ def dtype_of(precision: str):
     return PRECISIONS[precision]
 
 
-def exec_struct(device=0, n_shards=1, shard=0, row_block=4, precision="f64", devices=None, encode=None):
+def exec_struct(device=0, n_shards=1, shard=0, row_block=4, precision="f64", devices=None, encode=None,
+                solo=False):
     """rt_exec: the row shard, the precision, (rt_render only) a device list and an 8-bit output
-    encoding (None: linear RGB; "srgb": writeImage's codes; "sqrt": writeImageSqrt's)."""
+    encoding (None: linear RGB; "srgb": writeImage's codes; "sqrt": writeImageSqrt's); `solo`
+    (rt_render_async): the render does not overlap another on its device (RT_EXEC_SOLO)."""
     dtype_of(precision)
     if encode not in ENCODINGS:
         raise ValueError(f"encode must be one of {sorted(k for k in ENCODINGS if k)} or None, not {encode!r}")
     e = RtExec()
     e.device, e.n_shards, e.shard, e.row_block = device, n_shards, shard, row_block
-    e.flags = (RT_EXEC_F32 if precision == "f32" else 0) | ENCODINGS[encode]
+    e.flags = (RT_EXEC_F32 if precision == "f32" else 0) | ENCODINGS[encode] | (RT_EXEC_SOLO if solo else 0)
     if devices:
         arr = (ctypes.c_int32 * len(devices))(*[int(d) for d in devices])
         e.n_devices, e.devices = len(devices), ctypes.cast(arr, ctypes.POINTER(ctypes.c_int32))

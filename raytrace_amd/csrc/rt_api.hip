@@ -220,6 +220,7 @@ template <class R>
 int render_async(const rt_device_scene* s, const rt_camera_settings* cs, uint64_t seed, const rt_exec* ex, R* d_out,
                  void* hip_stream, char* ws_given = nullptr, size_t ws_cap = 0, int frame_rows = 0, bool lone = false) {
   if (int rc = ensure_precision<R>(s)) return rc;
+  lone = lone || (ex && (ex->flags & RT_EXEC_SOLO));  // (the caller says this render runs alone)
   const DevArrays<R>& A = s->arrays<R>();
   KernelParamsT<R> P;
   std::memset(&P, 0, sizeof P);
@@ -287,7 +288,7 @@ bool exec_f32(const rt_exec* ex) { return ex && (ex->flags & RT_EXEC_F32) != 0; 
 
 // rt_exec.flags: known bits only, at most one 8-bit encoding
 int check_flags(const rt_exec* ex) {
-  const int known = RT_EXEC_F32 | RT_EXEC_ENCODE8_SRGB | RT_EXEC_ENCODE8_SQRT;
+  const int known = RT_EXEC_F32 | RT_EXEC_ENCODE8_SRGB | RT_EXEC_ENCODE8_SQRT | RT_EXEC_SOLO;
   if (ex->flags & ~known) return fail(RT_E_INVALID, "unknown rt_exec.flags bits 0x%x", ex->flags & ~known);
   if ((ex->flags & RT_EXEC_ENCODE8_SRGB) && (ex->flags & RT_EXEC_ENCODE8_SQRT))
     return fail(RT_E_INVALID, "rt_exec.flags: RT_EXEC_ENCODE8_SRGB and RT_EXEC_ENCODE8_SQRT are exclusive");

@@ -137,12 +137,13 @@ class DeviceScene:
         return dict(upload_ms=st.upload_ms, bvh_nodes=st.bvh_nodes, max_stack=st.max_stack)
 
     def render_async(self, settings: CameraSettings, seed, out_ptr: int, stream_ptr: int = 0, n_shards: int = 1,
-                     shard: int = 0, row_block: int = 4, precision: str = "f64"):
+                     shard: int = 0, row_block: int = 4, precision: str = "f64", solo: bool = False):
         """Enqueue a render into the device buffer at out_ptr (rows x width x 3 float64, or float32
-        with precision="f32")."""
+        with precision="f32").  Renders are planned for frames that overlap on two or more streams;
+        `solo`: this one runs alone on its device (RT_EXEC_SOLO, the synchronous call's plan)."""
         cs = _lib.camera_struct(settings)
         ex = _lib.exec_struct(device=self.device, n_shards=n_shards, shard=shard, row_block=row_block,
-                              precision=precision)
+                              precision=precision, solo=solo)
         _lib.check(self._lib.rt_render_async(self.handle, ctypes.byref(cs), _seed64(seed), ctypes.byref(ex),
                                              ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream_ptr or None)))
 

@@ -177,6 +177,12 @@ def test_exec_flags_validated_before_device():
         ex.flags = flags
         assert L.rt_render(ctypes.byref(c), ctypes.byref(sc), 1, ctypes.byref(ex), out.ctypes.data, None) == _lib.RT_E_INVALID
         assert msg in L.rt_last_error(), (flags, L.rt_last_error())
+    # RT_EXEC_SOLO is a known bit: the call gets past the flag check (and then fails only for want
+    # of a device here, or renders on a GPU box)
+    ex = _lib.exec_struct(solo=True)
+    assert ex.flags == _lib.RT_EXEC_SOLO == 8
+    rc = L.rt_render(ctypes.byref(c), ctypes.byref(sc), 1, ctypes.byref(ex), out.ctypes.data, None)
+    assert rc != _lib.RT_E_INVALID or b"unknown" not in L.rt_last_error(), L.rt_last_error()
 
 
 def test_haskell_binding_offsets_match_header():

@@ -772,6 +772,16 @@ def test_device_scene_async_and_encode8_bit_exact(gpu, precision):
     ds.render_async(cs, seed, out.data_ptr(), s.cuda_stream, precision=precision)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(out.cpu().numpy(), R.raytrace(cs, world, seed, precision=precision))
+    # RT_EXEC_SOLO (the synchronous call's work plan) renders the same bytes
+    out2 = torch.full_like(out, float("nan"))
+    ds.render_async(cs, seed, out2.data_ptr(), s.cuda_stream, precision=precision, solo=True)
+    torch.cuda.synchronize()
+    assert torch.equal(out2, out)
+    big, bseed = cs.replace(cs_samplesPerPixel=200), seed  # (a frame with big items in both plans)
+    for solo in (False, True):
+        ds.render_async(big, bseed, (out if solo else out2).data_ptr(), s.cuda_stream, precision=precision, solo=solo)
+    torch.cuda.synchronize()
+    assert torch.equal(out2, out)
     # the render plus every code boundary (the host thresholds and their neighbours), NaN, +-inf,
     # negative and > 1 values: the device codes equal the host encoder's bit for bit
     x = np.linspace(0.0, 1.0, 4097)

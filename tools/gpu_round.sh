@@ -65,7 +65,7 @@ PY
           for ctr in FETCH_SIZE WRITE_SIZE; do
             d=$OUT/${c}_${p}_${nm}_$ctr
             timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $d -o run -- \
-              python3 bench.py --config $c --precision $p --no-f32 --steps 3 --warmup 1 --warmup-s 0 --no-cpu-baseline --streams 1 \
+              python3 bench.py --config $c --precision $p --no-f32 --steps 3 --warmup 1 --warmup-s 0 --no-cpu-baseline --streams 1 --plan overlapped \
               > $d.json 2> $d.err || { echo "pass $c $p $nm $ctr failed"; tail -3 $d.err; exit 1; }
             python3 - "$d" "$c $p $nm $ctr" <<'PY'
 import csv, glob, sys

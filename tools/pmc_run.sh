@@ -7,7 +7,7 @@
 set -o pipefail
 OUT=$1; CFG=${2:-cornell}; PREC=${3:-f64}
 mkdir -p "$OUT"; export TMPDIR=/tmp
-ARGS="--config $CFG --precision $PREC --no-f32 --steps 3 --warmup 1 --warmup-s 0 --no-cpu-baseline --streams 1"
+ARGS="--config $CFG --precision $PREC --no-f32 --steps 3 --warmup 1 --warmup-s 0 --no-cpu-baseline --streams 1 --plan overlapped"
 i=0
 for grp in "SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT" \
            "SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU" \
